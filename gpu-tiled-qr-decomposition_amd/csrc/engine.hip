@@ -1,0 +1,701 @@
+// MI355X tiled-QR engine: wave-batched kernels over the static DAG plan, plans, C ABI.
+//
+// Execution model (DESIGN.md "Engine"): the host scheduler (sched.c) turns the reference DAG
+// (src/gridscheduler.c) into BFS waves; every wave is two launches on two HIP streams —
+//   * panel kernel:  one 256-thread workgroup per GEQRT / TSQRT task (critical path),
+//   * update kernel: one 256-thread workgroup per 64-column strip of every UNMQR / TSMQR
+//     task of the wave (the bulk of the flops),
+// joined by events before the next wave. Tasks inside a wave are independent by
+// construction, so no intra-launch synchronisation is needed.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <new>
+#include <tuple>
+#include <vector>
+
+#include "gridscheduler.h"
+#include "tiles.hpp"
+#include "tqr.h"
+
+namespace tqr {
+
+// item = {type | strip << 8, l, m, k}  (reference Task fields, gridscheduler.h:13-17)
+struct Item {
+  int ts, l, m, k;
+};
+
+struct Args {
+  void* A;        // matrix (S*)
+  void* tau;      // compact tau (S*), m x kmax
+  double* Tw;     // T factors: [(k*p + i)*NG + g][IB*IB]
+  const Item* items;
+  long ldm;
+  int m, p, kmax;
+};
+
+template <int B>
+__device__ __forceinline__ double* tw_ptr(const Args& a, int i, int k, int g) {
+  using G = Geo<B>;
+  return a.Tw + (((size_t)k * a.p + i) * G::NG + g) * (G::IB * G::IB);
+}
+
+// ---------------------------------------------------------------------------------------
+// Panel kernel: GEQRT (QRS) and TSQRT (QRD) tasks, one workgroup each.
+// ---------------------------------------------------------------------------------------
+template <int B, typename S>
+__global__ __launch_bounds__(NT, 1) void k_panel(Args a) {
+  using G = Geo<B>;
+  constexpr int IB = G::IB, VP = G::VP, TP = G::TP, NG = G::NG;
+  extern __shared__ __align__(16) double lds[];
+  double* Vs = lds;
+  double* Hs = Vs + G::VSZ;
+  double* Ts = Hs + G::TSZ;
+  double* Gs = Ts + G::TSZ;
+  double* tauv = Gs + G::TSZ;
+  double* scratch = tauv + IB + 2;
+
+  const Item it = a.items[blockIdx.x];
+  const int type = it.ts & 0xff, l = it.l, k = it.k;
+  S* A = (S*)a.A;
+  S* tau = (S*)a.tau;
+  const size_t ldm = a.ldm;
+  const int t = threadIdx.x, w = t >> 6;
+  S* Rt = A + (size_t)k * B * ldm + (size_t)k * B;  // tile (k,k)
+  double X[G::NKS];
+  double H[G::NRI];
+
+  if (type == QRS) {
+    for (int g = 0; g < NG; ++g) {
+      const int c0 = g * IB, ks0 = c0 / 4;
+      for (int idx = t; idx < B * IB; idx += NT) {
+        int r = idx % B, c = idx / B;
+        Vs[r * VP + G::pc(c)] = r >= c0 ? ld(Rt + (size_t)(c0 + c) * ldm + r) : 0.0;
+      }
+      __syncthreads();
+      panel_factor<B, false>(Vs, Hs, tauv, scratch, c0);
+      // write back R / V of the panel, taus; then make V explicit (0 above, 1 on the diagonal)
+      for (int idx = t; idx < B * IB; idx += NT) {
+        int r = idx % B, c = idx / B, d = c0 + c;
+        double v = Vs[r * VP + G::pc(c)];
+        if (r >= c0) st(Rt + (size_t)d * ldm + r, v);
+      }
+      if (t < IB) st(tau + (size_t)k * a.m + (size_t)k * B + c0 + t, tauv[t]);
+      __syncthreads();
+      for (int idx = t; idx < B * IB; idx += NT) {
+        int r = idx % B, c = idx / B, d = c0 + c;
+        if (r <= d) Vs[r * VP + G::pc(c)] = r == d ? 1.0 : 0.0;
+      }
+      __syncthreads();
+      build_t<B>(Vs, tauv, Gs, Ts, ks0);
+      double* tg = tw_ptr<B>(a, k, k, g);
+      for (int idx = t; idx < IB * IB; idx += NT) tg[idx] = Ts[(idx / IB) * TP + idx % IB];
+      // trailing columns of the tile
+      const int nstr = (B - c0 - IB) / 16;
+      for (int s = w; s < nstr; s += NT / 64) {
+        const int col = c0 + IB + 16 * s;
+        load_strip<B>(X, Rt, ldm, col, ks0);
+        apply_group<B, false>(Vs, Ts, X, H, ks0);
+        store_strip<B>(X, Rt, ldm, col, ks0);
+      }
+      __syncthreads();
+    }
+  } else {  // QRD: TSQRT of [R_kk ; tile (l,k)]
+    S* Bt = A + (size_t)k * B * ldm + (size_t)l * B;
+    for (int g = 0; g < NG; ++g) {
+      const int c0 = g * IB;
+      for (int idx = t; idx < B * IB; idx += NT) {
+        int r = idx % B, c = idx / B;
+        Vs[r * VP + G::pc(c)] = ld(Bt + (size_t)(c0 + c) * ldm + r);
+      }
+      for (int idx = t; idx < IB * IB; idx += NT) {
+        int r = idx % IB, c = idx / IB;
+        if (r <= c) Hs[r * TP + c] = ld(Rt + (size_t)(c0 + c) * ldm + c0 + r);
+      }
+      __syncthreads();
+      panel_factor<B, true>(Vs, Hs, tauv, scratch, c0);
+      for (int idx = t; idx < B * IB; idx += NT) {
+        int r = idx % B, c = idx / B;
+        st(Bt + (size_t)(c0 + c) * ldm + r, Vs[r * VP + G::pc(c)]);
+      }
+      for (int idx = t; idx < IB * IB; idx += NT) {
+        int r = idx % IB, c = idx / IB;
+        if (r <= c) st(Rt + (size_t)(c0 + c) * ldm + c0 + r, Hs[r * TP + c]);
+      }
+      if (t < IB) st(tau + (size_t)k * a.m + (size_t)l * B + c0 + t, tauv[t]);
+      __syncthreads();
+      build_t<B>(Vs, tauv, Gs, Ts, 0);
+      double* tg = tw_ptr<B>(a, l, k, g);
+      for (int idx = t; idx < IB * IB; idx += NT) tg[idx] = Ts[(idx / IB) * TP + idx % IB];
+      const int nstr = (B - c0 - IB) / 16;
+      for (int s = w; s < nstr; s += NT / 64) {
+        const int col = c0 + IB + 16 * s;
+        load_strip<B>(X, Bt, ldm, col, 0);
+        load_head<B>(H, Rt, ldm, c0, col);
+        apply_group<B, true>(Vs, Ts, X, H, 0);
+        store_strip<B>(X, Bt, ldm, col, 0);
+        store_head<B>(H, Rt, ldm, c0, col);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Update kernel: UNMQR (SAPP) and TSMQR (DAPP) on one 64-column strip, one workgroup each;
+// wave w owns columns strip*64 + 16w .. +15 of the target tile(s).
+// ---------------------------------------------------------------------------------------
+template <int B, typename S>
+__global__ __launch_bounds__(NT, 2) void k_update(Args a) {
+  using G = Geo<B>;
+  constexpr int IB = G::IB, NG = G::NG;
+  extern __shared__ __align__(16) double lds[];
+  double* Vs = lds;
+  double* Ts = Vs + G::VSZ;
+
+  const Item it = a.items[blockIdx.x];
+  const int type = it.ts & 0xff, strip = it.ts >> 8, l = it.l, j = it.m, k = it.k;
+  S* A = (S*)a.A;
+  const size_t ldm = a.ldm;
+  const int w = threadIdx.x >> 6;
+  const int col = strip * 64 + 16 * w;  // strip column inside the tile
+  const bool active = col < B;
+  double X[G::NKS];
+  double H[G::NRI];
+
+  if (type == DAPP) {
+    const S* Vt = A + (size_t)k * B * ldm + (size_t)l * B;  // tile (l,k): V_B
+    S* At = A + (size_t)j * B * ldm + (size_t)k * B;        // tile (k,j): head rows
+    S* Bt = A + (size_t)j * B * ldm + (size_t)l * B;        // tile (l,j)
+    if (active) load_strip<B>(X, Bt, ldm, col, 0);
+    for (int g = 0; g < NG; ++g) {
+      __syncthreads();
+      stage_v_ts<B>(Vs, Vt, ldm, g * IB);
+      stage_t<B>(Ts, tw_ptr<B>(a, l, k, g));
+      __syncthreads();
+      if (active) {
+        load_head<B>(H, At, ldm, g * IB, col);
+        apply_group<B, true>(Vs, Ts, X, H, 0);
+        store_head<B>(H, At, ldm, g * IB, col);
+      }
+    }
+    if (active) store_strip<B>(X, Bt, ldm, col, 0);
+  } else {  // SAPP
+    const S* Vt = A + (size_t)k * B * ldm + (size_t)k * B;  // tile (k,k)
+    S* Ct = A + (size_t)j * B * ldm + (size_t)k * B;        // tile (k,j)
+    if (active) load_strip<B>(X, Ct, ldm, col, 0);
+    for (int g = 0; g < NG; ++g) {
+      __syncthreads();
+      stage_v_ge<B>(Vs, Vt, ldm, g * IB);
+      stage_t<B>(Ts, tw_ptr<B>(a, k, k, g));
+      __syncthreads();
+      if (active) apply_group<B, false>(Vs, Ts, X, H, g * IB / 4);
+    }
+    if (active) store_strip<B>(X, Ct, ldm, col, 0);
+  }
+}
+
+// T factors from a stored V and tau (for the single-tile API, where the caller hands over V
+// and tau as the reference's SLARFT/SSSRFT take them). One workgroup per (item, group).
+template <int B, typename S>
+__global__ __launch_bounds__(NT, 1) void k_build_t(Args a) {
+  using G = Geo<B>;
+  constexpr int IB = G::IB, NG = G::NG, TP = G::TP;
+  extern __shared__ __align__(16) double lds[];
+  double* Vs = lds;
+  double* Ts = Vs + G::VSZ;
+  double* Gs = Ts + G::TSZ;
+  double* tauv = Gs + G::TSZ;
+  const Item it = a.items[blockIdx.x / NG];
+  const int g = blockIdx.x % NG, c0 = g * IB, type = it.ts & 0xff, l = it.l, k = it.k;
+  const S* A = (const S*)a.A;
+  const S* tau = (const S*)a.tau;
+  const size_t ldm = a.ldm;
+  const int row0 = type == QRS ? k * B : l * B;
+  if (type == QRS) stage_v_ge<B>(Vs, A + (size_t)k * B * ldm + (size_t)k * B, ldm, c0);
+  else stage_v_ts<B>(Vs, A + (size_t)k * B * ldm + (size_t)l * B, ldm, c0);
+  if (threadIdx.x < IB) tauv[threadIdx.x] = ld(tau + (size_t)k * a.m + row0 + c0 + threadIdx.x);
+  __syncthreads();
+  build_t<B>(Vs, tauv, Gs, Ts, type == QRS ? c0 / 4 : 0);
+  double* tg = tw_ptr<B>(a, type == QRS ? k : l, k, g);
+  for (int idx = threadIdx.x; idx < IB * IB; idx += NT) tg[idx] = Ts[(idx / IB) * TP + idx % IB];
+}
+
+// RANDZO-distributed synthetic input: ((h mod 201) - 100) / 100 from a splitmix64 hash.
+template <typename S>
+__global__ void k_randzo(S* A, int m, int n, long ldm, unsigned long long seed) {
+  long total = (long)m * n;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long jj = e / m, ii = e % m;
+    unsigned long long z = seed * 0x9E3779B97F4A7C15ull + (unsigned long long)e + 0x632BE59BD9B4E019ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    A[jj * ldm + ii] = (S)(((double)(long)(z % 201ull) - 100.0) / 100.0);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------------
+static size_t lds_panel(int b) {
+  int ib = b < 32 ? b : 32;
+  size_t d = (size_t)b * (ib + 2) + 3 * (size_t)ib * (ib + 1) + (ib + 2) + 8 * 33 + 2 * (ib + 1) + 4;
+  return d * sizeof(double);
+}
+static size_t lds_update(int b) {
+  int ib = b < 32 ? b : 32;
+  return ((size_t)b * (ib + 2) + (size_t)ib * (ib + 1)) * sizeof(double);
+}
+
+typedef void (*kfn)(Args);
+template <int B, typename S>
+static void get_kernels(kfn* p, kfn* u, kfn* t) {
+  *p = k_panel<B, S>;
+  *u = k_update<B, S>;
+  *t = k_build_t<B, S>;
+}
+static size_t lds_build_t(int b) {
+  int ib = b < 32 ? b : 32;
+  return ((size_t)b * (ib + 2) + 2 * (size_t)ib * (ib + 1) + ib + 2) * sizeof(double);
+}
+// Resolve the kernels of one (b, dtype) and raise their dynamic-LDS limits.
+static int resolve(int b, int dtype, kfn* kp, kfn* ku, kfn* kt) {
+#define TQR_K(BB)                                                   \
+  case BB:                                                          \
+    if (dtype == TQR_F64) get_kernels<BB, double>(kp, ku, kt);      \
+    else get_kernels<BB, float>(kp, ku, kt);                        \
+    break;
+  switch (b) { TQR_K(16) TQR_K(32) TQR_K(64) TQR_K(128) TQR_K(256) default: return TQR_EINVAL; }
+#undef TQR_K
+  if (hipFuncSetAttribute((const void*)*kp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_panel(b)) != hipSuccess ||
+      hipFuncSetAttribute((const void*)*ku, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_update(b)) != hipSuccess ||
+      hipFuncSetAttribute((const void*)*kt, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_build_t(b)) != hipSuccess)
+    return TQR_EHIP;
+  return TQR_OK;
+}
+
+static bool valid_b(int b) { return b == 16 || b == 32 || b == 64 || b == 128 || b == 256; }
+
+}  // namespace tqr
+
+using namespace tqr;
+
+struct tqr_plan {
+  int m, n, b, p, q, kmax, dtype, nlevels;
+  size_t es;
+  std::vector<long> off_p, off_u;  // per wave offsets into the item arrays
+  Item* d_items_p = nullptr;
+  Item* d_items_u = nullptr;
+  double* d_T = nullptr;
+  hipStream_t sP = nullptr, sU = nullptr;
+  hipEvent_t evP = nullptr, evU = nullptr, evStart = nullptr;
+  kfn kp = nullptr, ku = nullptr;
+  size_t ldsP = 0, ldsU = 0;
+  int profile = 0;
+  std::vector<hipEvent_t> prof_ev;  // pairs per launch when profiling
+  std::vector<int> prof_kind;
+  int nl_u = 0, nl_p = 0;
+  double ms_u = 0, ms_p = 0;
+};
+
+#define HIPCHK(x)                                                                         \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      fprintf(stderr, "tqr: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      return TQR_EHIP;                                                                    \
+    }                                                                                     \
+  } while (0)
+
+extern "C" {
+
+const char* tqr_strerror(int s) {
+  switch (s) {
+    case TQR_OK: return "ok";
+    case TQR_EINVAL: return "invalid argument";
+    case TQR_ENOMEM: return "out of memory";
+    case TQR_EHIP: return "HIP runtime error";
+    case TQR_ENODEV: return "no usable gfx950 device";
+    case TQR_ERCCL: return "RCCL error";
+  }
+  return "unknown";
+}
+
+const char* tqr_version(void) { return "tqr 0.1 (gfx950, flat-tree tiled Householder QR)"; }
+
+long tqr_total_tasks(int m, int n, int b) {
+  if (b <= 0 || m % b || n % b) return -1;
+  return tqr_sched_total_tasks(m / b, n / b);
+}
+
+static int check_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return TQR_ENODEV;
+  hipDeviceProp_t pr;
+  if (hipGetDeviceProperties(&pr, dev) != hipSuccess) return TQR_ENODEV;
+  if (strncmp(pr.gcnArchName, "gfx950", 6) != 0) {
+    fprintf(stderr, "tqr: device %d is %s, this build targets gfx950 only\n", dev, pr.gcnArchName);
+    return TQR_ENODEV;
+  }
+  return TQR_OK;
+}
+
+void tqr_plan_destroy(tqr_plan* pl) {
+  if (!pl) return;
+  if (pl->d_items_p) (void)hipFree(pl->d_items_p);
+  if (pl->d_items_u) (void)hipFree(pl->d_items_u);
+  if (pl->d_T) (void)hipFree(pl->d_T);
+  if (pl->sP) (void)hipStreamDestroy(pl->sP);
+  if (pl->sU) (void)hipStreamDestroy(pl->sU);
+  if (pl->evP) (void)hipEventDestroy(pl->evP);
+  if (pl->evU) (void)hipEventDestroy(pl->evU);
+  if (pl->evStart) (void)hipEventDestroy(pl->evStart);
+  for (auto e : pl->prof_ev) (void)hipEventDestroy(e);
+  delete pl;
+}
+
+int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) {
+  if (!out) return TQR_EINVAL;
+  *out = nullptr;
+  if (!valid_b(b) || m <= 0 || n <= 0 || m % b || n % b || (dtype != TQR_F32 && dtype != TQR_F64))
+    return TQR_EINVAL;
+  int st = check_device();
+  if (st) return st;
+  tqr_plan* pl = new (std::nothrow) tqr_plan();
+  if (!pl) return TQR_ENOMEM;
+  pl->m = m; pl->n = n; pl->b = b; pl->p = m / b; pl->q = n / b;
+  pl->kmax = std::min(pl->p, pl->q);
+  pl->dtype = dtype;
+  pl->es = dtype == TQR_F64 ? 8 : 4;
+
+  tqr_plan_t sp;
+  if (tqr_sched_plan(pl->p, pl->q, &sp) != 0) { delete pl; return TQR_ENOMEM; }
+  pl->nlevels = sp.nlevels;
+  const int nstrips = (b + 63) / 64;
+  std::vector<Item> ip, iu;
+  ip.reserve(sp.ntasks);
+  iu.reserve(sp.ntasks * nstrips);
+  for (int L = 0; L < sp.nlevels; ++L) {
+    pl->off_p.push_back((long)ip.size());
+    pl->off_u.push_back((long)iu.size());
+    for (long x = sp.level_off[L]; x < sp.level_off[L + 1]; ++x) {
+      const int* tk = sp.tasks + 4 * x;
+      if (tk[0] == QRS || tk[0] == QRD) {
+        ip.push_back(Item{tk[0], tk[1], tk[2], tk[3]});
+      } else {
+        for (int s = 0; s < nstrips; ++s) iu.push_back(Item{tk[0] | (s << 8), tk[1], tk[2], tk[3]});
+      }
+    }
+  }
+  pl->off_p.push_back((long)ip.size());
+  pl->off_u.push_back((long)iu.size());
+  tqr_sched_plan_free(&sp);
+
+  int ib = b < 32 ? b : 32;
+  size_t tw = (size_t)pl->p * pl->kmax * (b / ib) * ib * ib * sizeof(double);
+  if (hipMalloc(&pl->d_items_p, std::max<size_t>(1, ip.size()) * sizeof(Item)) != hipSuccess ||
+      hipMalloc(&pl->d_items_u, std::max<size_t>(1, iu.size()) * sizeof(Item)) != hipSuccess ||
+      hipMalloc(&pl->d_T, tw) != hipSuccess) {
+    tqr_plan_destroy(pl);
+    return TQR_ENOMEM;
+  }
+  if (!ip.empty() && hipMemcpy(pl->d_items_p, ip.data(), ip.size() * sizeof(Item), hipMemcpyHostToDevice) != hipSuccess) {
+    tqr_plan_destroy(pl); return TQR_EHIP;
+  }
+  if (!iu.empty() && hipMemcpy(pl->d_items_u, iu.data(), iu.size() * sizeof(Item), hipMemcpyHostToDevice) != hipSuccess) {
+    tqr_plan_destroy(pl); return TQR_EHIP;
+  }
+  if (hipStreamCreateWithFlags(&pl->sP, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&pl->sU, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&pl->evP, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&pl->evU, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&pl->evStart, hipEventDisableTiming) != hipSuccess) {
+    tqr_plan_destroy(pl); return TQR_EHIP;
+  }
+kfn kt;
+  if (resolve(b, dtype, &pl->kp, &pl->ku, &kt) != TQR_OK) { tqr_plan_destroy(pl); return TQR_EHIP; }
+  pl->ldsP = lds_panel(b);
+  pl->ldsU = lds_update(b);
+  *out = pl;
+  return TQR_OK;
+}
+
+int tqr_plan_set_profile(tqr_plan* pl, int on) {
+  if (!pl) return TQR_EINVAL;
+  pl->profile = on;
+  return TQR_OK;
+}
+
+int tqr_plan_stats(const tqr_plan* pl, int* nu, double* msu, int* np, double* msp) {
+  if (!pl) return TQR_EINVAL;
+  if (nu) *nu = pl->nl_u;
+  if (msu) *msu = pl->ms_u;
+  if (np) *np = pl->nl_p;
+  if (msp) *msp = pl->ms_p;
+  return TQR_OK;
+}
+
+int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream) {
+  if (!pl || !dA || !dtau || ldda < pl->m) return TQR_EINVAL;
+  hipStream_t cs = (hipStream_t)stream;
+  Args a;
+  a.A = dA; a.tau = dtau; a.Tw = pl->d_T; a.ldm = ldda; a.m = pl->m; a.p = pl->p; a.kmax = pl->kmax;
+  // both work streams start after everything already queued on the caller's stream
+  HIPCHK(hipEventRecord(pl->evStart, cs));
+  HIPCHK(hipStreamWaitEvent(pl->sP, pl->evStart, 0));
+  HIPCHK(hipStreamWaitEvent(pl->sU, pl->evStart, 0));
+  HIPCHK(hipEventRecord(pl->evP, pl->sP));
+  HIPCHK(hipEventRecord(pl->evU, pl->sU));
+  size_t nev = 0;
+  if (pl->profile) {
+    size_t need = 2 * (size_t)pl->nlevels * 2;
+    while (pl->prof_ev.size() < need) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      pl->prof_ev.push_back(e);
+    }
+    pl->prof_kind.assign(need / 2, -1);
+  }
+  for (int L = 0; L < pl->nlevels; ++L) {
+    long np = pl->off_p[L + 1] - pl->off_p[L];
+    long nu = pl->off_u[L + 1] - pl->off_u[L];
+    // each stream waits for the other stream's previous wave (events hold wave L-1)
+    HIPCHK(hipStreamWaitEvent(pl->sP, pl->evU, 0));
+    HIPCHK(hipStreamWaitEvent(pl->sU, pl->evP, 0));
+    if (np) {
+      a.items = pl->d_items_p + pl->off_p[L];
+      if (pl->profile) { pl->prof_kind[nev / 2] = 1; HIPCHK(hipEventRecord(pl->prof_ev[nev++], pl->sP)); }
+      hipLaunchKernelGGL(pl->kp, dim3((unsigned)np), dim3(NT), pl->ldsP, pl->sP, a);
+      HIPCHK(hipGetLastError());
+      if (pl->profile) HIPCHK(hipEventRecord(pl->prof_ev[nev++], pl->sP));
+    }
+    if (nu) {
+      a.items = pl->d_items_u + pl->off_u[L];
+      if (pl->profile) { pl->prof_kind[nev / 2] = 0; HIPCHK(hipEventRecord(pl->prof_ev[nev++], pl->sU)); }
+      hipLaunchKernelGGL(pl->ku, dim3((unsigned)nu), dim3(NT), pl->ldsU, pl->sU, a);
+      HIPCHK(hipGetLastError());
+      if (pl->profile) HIPCHK(hipEventRecord(pl->prof_ev[nev++], pl->sU));
+    }
+    HIPCHK(hipEventRecord(pl->evP, pl->sP));
+    HIPCHK(hipEventRecord(pl->evU, pl->sU));
+  }
+  HIPCHK(hipStreamWaitEvent(cs, pl->evP, 0));
+  HIPCHK(hipStreamWaitEvent(cs, pl->evU, 0));
+  if (pl->profile) {
+    HIPCHK(hipStreamSynchronize(cs));
+    pl->nl_u = pl->nl_p = 0;
+    pl->ms_u = pl->ms_p = 0;
+    for (size_t x = 0; x + 1 < nev; x += 2) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, pl->prof_ev[x], pl->prof_ev[x + 1]));
+      if (pl->prof_kind[x / 2] == 1) { pl->nl_p++; pl->ms_p += ms; }
+      else { pl->nl_u++; pl->ms_u += ms; }
+    }
+  }
+  return TQR_OK;
+}
+
+// ---- plan cache for the one-shot helpers -------------------------------------------------
+static std::mutex g_cache_mu;
+static std::map<std::tuple<int, int, int, int, int>, tqr_plan*> g_cache;
+
+static int cached_plan(int m, int n, int b, int dtype, tqr_plan** out) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return TQR_ENODEV;
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  auto key = std::make_tuple(dev, m, n, b, dtype);
+  auto itc = g_cache.find(key);
+  if (itc != g_cache.end()) { *out = itc->second; return TQR_OK; }
+  int st = tqr_plan_create(out, m, n, b, dtype);
+  if (st == TQR_OK) g_cache[key] = *out;
+  return st;
+}
+
+int tqr_dgeqrt_tiled(int m, int n, int b, double* dA, int ldda, double* dtau, void* stream) {
+  tqr_plan* pl;
+  int st = cached_plan(m, n, b, TQR_F64, &pl);
+  return st ? st : tqr_plan_execute(pl, dA, ldda, dtau, stream);
+}
+int tqr_sgeqrt_tiled(int m, int n, int b, float* dA, int ldda, float* dtau, void* stream) {
+  tqr_plan* pl;
+  int st = cached_plan(m, n, b, TQR_F32, &pl);
+  return st ? st : tqr_plan_execute(pl, dA, ldda, dtau, stream);
+}
+
+// Host-pointer factorisation: 2-D copies in, factorise, copies out, tau expanded to the
+// reference's m x n layout (column k*b of tau = compact column k).
+static int geqrt_host(void* A, void* tau, int m, int n, int ldm, int b, int dtype) {
+  if (!A || ldm < m || !valid_b(b) || m <= 0 || n <= 0 || m % b || n % b) return TQR_EINVAL;
+  tqr_plan* pl;
+  int st = cached_plan(m, n, b, dtype, &pl);
+  if (st) return st;
+  size_t es = dtype == TQR_F64 ? 8 : 4;
+  void *dA = nullptr, *dT = nullptr;
+  int kmax = std::min(m, n) / b;
+  if (hipMalloc(&dA, es * (size_t)m * n) != hipSuccess) return TQR_ENOMEM;
+  if (hipMalloc(&dT, es * (size_t)m * kmax) != hipSuccess) { (void)hipFree(dA); return TQR_ENOMEM; }
+  st = TQR_OK;
+  if (hipMemcpy2D(dA, es * m, A, es * ldm, es * m, n, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(dT, 0, es * (size_t)m * kmax) != hipSuccess) st = TQR_EHIP;
+  if (!st) st = tqr_plan_execute(pl, dA, m, dT, nullptr);
+  if (!st && hipDeviceSynchronize() != hipSuccess) st = TQR_EHIP;
+  if (!st && hipMemcpy2D(A, es * ldm, dA, es * m, es * m, n, hipMemcpyDeviceToHost) != hipSuccess) st = TQR_EHIP;
+  if (!st && tau) {
+    // column k of the compact array -> column k*b of the reference tau matrix, rows k*b..m-1
+    for (int k = 0; k < kmax && !st; ++k) {
+      char* dst = (char*)tau + es * ((size_t)k * b * ldm + (size_t)k * b);
+      const char* src = (const char*)dT + es * ((size_t)k * m + (size_t)k * b);
+      if (hipMemcpy(dst, src, es * (size_t)(m - k * b), hipMemcpyDeviceToHost) != hipSuccess) st = TQR_EHIP;
+    }
+  }
+  (void)hipFree(dA);
+  (void)hipFree(dT);
+  return st;
+}
+
+int tqr_dgeqrt_host(double* A, double* tau, int m, int n, int ldm, int b) { return geqrt_host(A, tau, m, n, ldm, b, TQR_F64); }
+int tqr_sgeqrt_host(float* A, float* tau, int m, int n, int ldm, int b) { return geqrt_host(A, tau, m, n, ldm, b, TQR_F32); }
+
+int tqr_fill_randzo(int dtype, void* dA, int m, int n, int ldda, unsigned long long seed, void* stream) {
+  if (!dA || ldda < m || m <= 0 || n <= 0) return TQR_EINVAL;
+  long total = (long)m * n;
+  int blocks = (int)std::min<long>(65536, (total + 255) / 256);
+  if (dtype == TQR_F64)
+    hipLaunchKernelGGL(k_randzo<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (double*)dA, m, n, (long)ldda, seed);
+  else
+    hipLaunchKernelGGL(k_randzo<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (float*)dA, m, n, (long)ldda, seed);
+  HIPCHK(hipGetLastError());
+  return TQR_OK;
+}
+
+}  // extern "C"
+
+// ---- single-tile API ----------------------------------------------------------------------
+// The tile(s) are copied into a small device matrix laid out as the corresponding corner of
+// a tiled matrix, the task runs as a one-item wave, and the result is copied back.
+namespace {
+struct TileRun {
+  int b, dtype, mr, nc;  // device matrix mr x nc (ld = mr)
+  size_t es;
+  void* dA = nullptr;
+  void* dtau = nullptr;
+  double* dT = nullptr;
+  Item* dit = nullptr;
+  kfn kp, ku, kt;
+  int init(int b_, int dtype_, int p, int q) {
+    b = b_; dtype = dtype_; mr = p * b; nc = q * b; es = dtype == TQR_F64 ? 8 : 4;
+    if (!valid_b(b) || (dtype != TQR_F64 && dtype != TQR_F32)) return TQR_EINVAL;
+    int st = check_device();
+    if (st) return st;
+    if ((st = resolve(b, dtype, &kp, &ku, &kt))) return st;
+    int ib = b < 32 ? b : 32;
+    if (hipMalloc(&dA, es * mr * nc) != hipSuccess || hipMalloc(&dtau, es * mr) != hipSuccess ||
+        hipMalloc(&dT, sizeof(double) * (size_t)p * b * ib) != hipSuccess || hipMalloc(&dit, sizeof(Item) * 4) != hipSuccess)
+      return TQR_ENOMEM;
+    if (hipMemset(dA, 0, es * mr * nc) != hipSuccess || hipMemset(dtau, 0, es * mr) != hipSuccess) return TQR_EHIP;
+    return TQR_OK;
+  }
+  ~TileRun() {
+    if (dA) (void)hipFree(dA);
+    if (dtau) (void)hipFree(dtau);
+    if (dT) (void)hipFree(dT);
+    if (dit) (void)hipFree(dit);
+  }
+  int put(const void* h, int ldm, int r, int c) {  // host tile -> device tile (r,c)
+    return hipMemcpy2D((char*)dA + es * ((size_t)c * b * mr + (size_t)r * b), es * mr, h, es * ldm, es * b, b,
+                       hipMemcpyHostToDevice) == hipSuccess ? TQR_OK : TQR_EHIP;
+  }
+  int get(void* h, int ldm, int r, int c) {
+    return hipMemcpy2D(h, es * ldm, (char*)dA + es * ((size_t)c * b * mr + (size_t)r * b), es * mr, es * b, b,
+                       hipMemcpyDeviceToHost) == hipSuccess ? TQR_OK : TQR_EHIP;
+  }
+  int put_tau(const void* h, int row0) {
+    return hipMemcpy((char*)dtau + es * row0, h, es * b, hipMemcpyHostToDevice) == hipSuccess ? TQR_OK : TQR_EHIP;
+  }
+  int get_tau(void* h, int row0) {
+    return hipMemcpy(h, (char*)dtau + es * row0, es * b, hipMemcpyDeviceToHost) == hipSuccess ? TQR_OK : TQR_EHIP;
+  }
+  int run(kfn k, Item item, int grid, size_t lds) {
+    if (hipMemcpy(dit, &item, sizeof item, hipMemcpyHostToDevice) != hipSuccess) return TQR_EHIP;
+    Args a;
+    a.A = dA; a.tau = dtau; a.Tw = dT; a.items = dit; a.ldm = mr; a.m = mr; a.p = mr / b; a.kmax = 1;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, 0, a);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return TQR_EHIP;
+    return TQR_OK;
+  }
+  int ng() const { return b / (b < 32 ? b : 32); }
+  int nstrips() const { return (b + 63) / 64; }
+  int run_update(Item item) {
+    for (int s = 0; s < nstrips(); ++s) {
+      Item it2 = item;
+      it2.ts |= s << 8;
+      int st = run(ku, it2, 1, lds_update(b));
+      if (st) return st;
+    }
+    return TQR_OK;
+  }
+};
+}  // namespace
+
+extern "C" {
+
+int tqr_tile_geqrt(int dtype, void* blk, void* tau, int b, int ldm) {
+  if (!blk || !tau || ldm < b) return TQR_EINVAL;
+  TileRun tr;
+  int st = tr.init(b, dtype, 1, 1);
+  if (!st) st = tr.put(blk, ldm, 0, 0);
+  if (!st) st = tr.run(tr.kp, Item{QRS, 0, 0, 0}, 1, lds_panel(b));
+  if (!st) st = tr.get(blk, ldm, 0, 0);
+  if (!st) st = tr.get_tau(tau, 0);
+  return st;
+}
+
+int tqr_tile_unmqr(int dtype, void* C, const void* V, const void* tau, int b, int ldm) {
+  if (!C || !V || !tau || ldm < b) return TQR_EINVAL;
+  TileRun tr;
+  int st = tr.init(b, dtype, 1, 2);
+  if (!st) st = tr.put(V, ldm, 0, 0);
+  if (!st) st = tr.put(C, ldm, 0, 1);
+  if (!st) st = tr.put_tau(tau, 0);
+  if (!st) st = tr.run(tr.kt, Item{QRS, 0, 0, 0}, tr.ng(), lds_build_t(b));
+  if (!st) st = tr.run_update(Item{SAPP, 0, 1, 0});
+  if (!st) st = tr.get(C, ldm, 0, 1);
+  return st;
+}
+
+int tqr_tile_tsqrt(int dtype, void* A, void* Bm, void* tau, int b, int ldm) {
+  if (!A || !Bm || !tau || ldm < b) return TQR_EINVAL;
+  TileRun tr;
+  int st = tr.init(b, dtype, 2, 1);
+  if (!st) st = tr.put(A, ldm, 0, 0);
+  if (!st) st = tr.put(Bm, ldm, 1, 0);
+  if (!st) st = tr.run(tr.kp, Item{QRD, 1, 0, 0}, 1, lds_panel(b));
+  if (!st) st = tr.get(A, ldm, 0, 0);
+  if (!st) st = tr.get(Bm, ldm, 1, 0);
+  if (!st) st = tr.get_tau(tau, b);
+  return st;
+}
+
+int tqr_tile_tsmqr(int dtype, const void* V, void* A, void* Bm, const void* tau, int b, int ldm) {
+  if (!V || !A || !Bm || !tau || ldm < b) return TQR_EINVAL;
+  TileRun tr;
+  int st = tr.init(b, dtype, 2, 2);
+  if (!st) st = tr.put(V, ldm, 1, 0);
+  if (!st) st = tr.put(A, ldm, 0, 1);
+  if (!st) st = tr.put(Bm, ldm, 1, 1);
+  if (!st) st = tr.put_tau(tau, b);
+  if (!st) st = tr.run(tr.kt, Item{QRD, 1, 0, 0}, tr.ng(), lds_build_t(b));
+  if (!st) st = tr.run_update(Item{DAPP, 1, 1, 0});
+  if (!st) st = tr.get(A, ldm, 0, 1);
+  if (!st) st = tr.get(Bm, ldm, 1, 1);
+  return st;
+}
+
+}  // extern "C"

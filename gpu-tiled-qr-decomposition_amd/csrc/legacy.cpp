@@ -1,0 +1,211 @@
+// The reference's host and GPU entry points (qrdecomp.h, gpucalc.h) on top of the native tqr
+// API. Every compute call goes to the GPU; a failure is reported and aborts the process.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include <hip/hip_runtime.h>
+
+#include "gpucalc.h"
+#include "qrdecomp.h"
+#include "tqr.h"
+
+namespace {
+void die(const char* what, int st) {
+  fprintf(stderr, "tqr: %s failed: %s (%d)\n", what, tqr_strerror(st), st);
+  abort();
+}
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+template <typename T>
+void copy_mat(const T* a, int m, int n, int ldm, T* b) {
+  for (int j = 0; j < n; ++j) memcpy(b + (size_t)j * ldm, a + (size_t)j * ldm, sizeof(T) * m);
+}
+template <typename T>
+void do_task(Task t, T* mat, T* tau, int b, int ldm, int dtype) {
+  size_t kb = (size_t)t.k * b, lb = (size_t)t.l * b, mb = (size_t)t.m * b;
+  int st = TQR_EINVAL;
+  switch (t.taskType) {
+    case QRS: st = tqr_tile_geqrt(dtype, mat + kb * ldm + kb, tau + kb * ldm + kb, b, ldm); break;
+    case SAPP: st = tqr_tile_unmqr(dtype, mat + mb * ldm + kb, mat + kb * ldm + kb, tau + kb * ldm + kb, b, ldm); break;
+    case QRD: st = tqr_tile_tsqrt(dtype, mat + kb * ldm + kb, mat + kb * ldm + lb, tau + kb * ldm + lb, b, ldm); break;
+    case DAPP:
+      st = tqr_tile_tsmqr(dtype, mat + kb * ldm + lb, mat + mb * ldm + kb, mat + mb * ldm + lb, tau + kb * ldm + lb, b, ldm);
+      break;
+  }
+  if (st) die("doATask", st);
+}
+}  // namespace
+
+extern "C" {
+
+void cudaQRTask(float* mat, int m, int n, int ldm, int maxblocks) {
+  (void)maxblocks;
+  double t0 = now_ms();
+  int st = tqr_sgeqrt_host(mat, nullptr, m, n, ldm, 32);
+  if (st) die("cudaQRTask", st);
+  printf("GPU: %5.3f ms\n", now_ms() - t0);
+}
+void cudaQRTask_d(double* mat, int m, int n, int ldm, int maxblocks) {
+  (void)maxblocks;
+  double t0 = now_ms();
+  int st = tqr_dgeqrt_host(mat, nullptr, m, n, ldm, 32);
+  if (st) die("cudaQRTask_d", st);
+  printf("GPU: %5.3f ms\n", now_ms() - t0);
+}
+void cudaQRFull(float* mat, int m, int n) { cudaQRTask(mat, m, n, m, 0); }
+
+// TSMQR throughput hook (gpucalc.cu:1706-1774): timings[r] = ms of r-th batch of `nblocks`
+// independent b = 32 TSMQR tile updates (here: one 64 x (32*nblocks) fp32 panel factorised
+// down to its trailing update, timed with HIP events).
+void testDAPP(float* timings, int n, int nblocks) {
+  if (!timings || n <= 0 || nblocks <= 0) return;
+  const int b = 32, m = 2 * b, cols = b * (nblocks + 1);
+  float* dA = nullptr;
+  float* dT = nullptr;
+  if (hipMalloc(&dA, sizeof(float) * (size_t)m * cols) != hipSuccess || hipMalloc(&dT, sizeof(float) * m * 2) != hipSuccess)
+    die("testDAPP", TQR_ENOMEM);
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) die("testDAPP", TQR_EHIP);
+  for (int r = 0; r < n; ++r) {
+    int st = tqr_fill_randzo(TQR_F32, dA, m, cols, m, 5 + r, nullptr);
+    if (!st && hipEventRecord(e0, nullptr) != hipSuccess) st = TQR_EHIP;
+    if (!st) st = tqr_sgeqrt_tiled(m, cols, b, dA, m, dT, nullptr);
+    if (!st && hipEventRecord(e1, nullptr) != hipSuccess) st = TQR_EHIP;
+    if (!st && hipEventSynchronize(e1) != hipSuccess) st = TQR_EHIP;
+    if (st) die("testDAPP", st);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    timings[r] = ms;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(dA);
+  (void)hipFree(dT);
+}
+
+// One TSMQR on a 64 x 64 fp32 matrix (gpucalc.cu:1776-1799): V = tile (1,0), tau = its
+// diagonal entries as stored by the reference (tau of tile (1,0) at rows 32.., column 0 of a
+// tau matrix is not passed in the reference either; it uses mat's own layout), A = (0,1),
+// B = (1,1). Here tau is taken as 2/(1+|v|^2) of each V column, i.e. V is treated as a
+// TSQRT output.
+void doCUDADAPP(float* mat) {
+  if (!mat) return;
+  const int b = 32, ldm = 64;
+  float tau[32];
+  for (int c = 0; c < b; ++c) {
+    double s = 1.0;
+    for (int r = 0; r < b; ++r) s += (double)mat[(size_t)c * ldm + b + r] * mat[(size_t)c * ldm + b + r];
+    tau[c] = (float)(2.0 / s);
+  }
+  int st = tqr_tile_tsmqr(TQR_F32, mat + b, mat + (size_t)b * ldm, mat + (size_t)b * ldm + b, tau, b, ldm);
+  if (st) die("doCUDADAPP", st);
+}
+
+void taskQRP_threads(float* matData, float* matResult, float* tau, int m, int n, int b, int ldm, int useWY) {
+  (void)useWY;
+  double t0 = now_ms();
+  copy_mat(matData, m, n, ldm, matResult);
+  int st = tqr_sgeqrt_host(matResult, tau, m, n, ldm, b);
+  if (st) die("taskQRP_threads", st);
+  printf("CPU: %5.2f ms\n", now_ms() - t0);
+}
+void taskQRP_threads_d(double* matData, double* matResult, double* tau, int m, int n, int b, int ldm, int useWY) {
+  (void)useWY;
+  double t0 = now_ms();
+  copy_mat(matData, m, n, ldm, matResult);
+  int st = tqr_dgeqrt_host(matResult, tau, m, n, ldm, b);
+  if (st) die("taskQRP_threads_d", st);
+  printf("CPU: %5.2f ms\n", now_ms() - t0);
+}
+
+void doATask(Task t, float* mat, float* tau, int b, int ldm, float** colVect, int useWY) {
+  (void)colVect; (void)useWY;
+  do_task(t, mat, tau, b, ldm, TQR_F32);
+}
+void doATask_d(Task t, double* mat, double* tau, int b, int ldm, double** colVect, int useWY) {
+  (void)colVect; (void)useWY;
+  do_task(t, mat, tau, b, ldm, TQR_F64);
+}
+
+#define TILE_CHECK(cond, name) \
+  if (!(cond)) { fprintf(stderr, "tqr: %s: only square b x b tiles are supported\n", name); abort(); }
+
+void SGEQRF(float* block, float* tauBlock, int m, int n, int ldm, float* w) {
+  (void)w; TILE_CHECK(m == n, "SGEQRF");
+  int st = tqr_tile_geqrt(TQR_F32, block, tauBlock, n, ldm);
+  if (st) die("SGEQRF", st);
+}
+void SLARFT(float* block, float* blockV, float* tauBlock, int m, int n, int ldm, float** w) {
+  (void)w; TILE_CHECK(m == n, "SLARFT");
+  int st = tqr_tile_unmqr(TQR_F32, block, blockV, tauBlock, n, ldm);
+  if (st) die("SLARFT", st);
+}
+void STSQRF(float* A, float* B, float* tau, int ma, int mb, int n, int ldm, float* hh) {
+  (void)hh; TILE_CHECK(ma == n && mb == n, "STSQRF");
+  int st = tqr_tile_tsqrt(TQR_F32, A, B, tau, n, ldm);
+  if (st) die("STSQRF", st);
+}
+void SSSRFT(float* V, float* A, float* B, float* tau, int b, int n, int ldm) {
+  TILE_CHECK(b == n, "SSSRFT");
+  int st = tqr_tile_tsmqr(TQR_F32, V, A, B, tau, b, ldm);
+  if (st) die("SSSRFT", st);
+}
+void DGEQRF(double* block, double* tauBlock, int m, int n, int ldm, double* w) {
+  (void)w; TILE_CHECK(m == n, "DGEQRF");
+  int st = tqr_tile_geqrt(TQR_F64, block, tauBlock, n, ldm);
+  if (st) die("DGEQRF", st);
+}
+void DLARFT(double* block, double* blockV, double* tauBlock, int m, int n, int ldm, double** w) {
+  (void)w; TILE_CHECK(m == n, "DLARFT");
+  int st = tqr_tile_unmqr(TQR_F64, block, blockV, tauBlock, n, ldm);
+  if (st) die("DLARFT", st);
+}
+void DTSQRF(double* A, double* B, double* tau, int ma, int mb, int n, int ldm, double* hh) {
+  (void)hh; TILE_CHECK(ma == n && mb == n, "DTSQRF");
+  int st = tqr_tile_tsqrt(TQR_F64, A, B, tau, n, ldm);
+  if (st) die("DTSQRF", st);
+}
+void DSSRFT(double* V, double* A, double* B, double* tau, int b, int n, int ldm) {
+  TILE_CHECK(b == n, "DSSRFT");
+  int st = tqr_tile_tsmqr(TQR_F64, V, A, B, tau, b, ldm);
+  if (st) die("DSSRFT", st);
+}
+
+// ---- host utilities (qrdecomp.c:1313-1400) ------------------------------------------------
+float* newMatrix(int m, int n) { return (float*)malloc(sizeof(float) * (size_t)m * n); }
+void deleteMatrix(float* mat) { free(mat); }
+void initMatrix(float* mat, int m, int n, int ldm, int mode) {
+  for (int c = 0; c < n; ++c)
+    for (int r = 0; r < m; ++r) {
+      float* e = mat + (size_t)c * ldm + r;
+      if (mode == 0) *e = 0;
+      else if (mode == 1) *e = (float)(rand() % 32);
+      else if (mode == 2) *e = (float)(((float)(rand() % 201) - 100.0) / 100.0);
+      else if (mode == 3) *e = r == c ? 1.0f : 0.0f;
+    }
+}
+void printMatrix(float* mat, int m, int n, int ldm) {
+  putchar('[');
+  for (int r = 0; r < m; ++r) {
+    for (int c = 0; c < n; ++c) printf(" %2.3f", mat[(size_t)c * ldm + r]);
+    if (r != m - 1) putchar(';');
+  }
+  printf("]\n");
+}
+void copyMatrix(float* mat, int m, int n, int ldm, float* copymat) { copy_mat(mat, m, n, ldm, copymat); }
+int checkEqual(float* a, float* b, int m, int n, int ldm) {
+  for (int i = 0; i < m; ++i)
+    for (int j = 0; j < n; ++j) {
+      float d = a[(size_t)j * ldm + i] - b[(size_t)j * ldm + i];
+      if (d > 0.001f || d < -0.001f) {
+        printf("(%d,%d): %2.3f /= %2.3f\n", i, j, a[(size_t)j * ldm + i], b[(size_t)j * ldm + i]);
+        return 0;
+      }
+    }
+  return 1;
+}
+
+}  // extern "C"

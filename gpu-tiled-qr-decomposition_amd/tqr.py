@@ -1,0 +1,227 @@
+"""Python host mirror of the MI355X tiled QR (libtqr.so) — thin ctypes bindings.
+
+The product is the C ABI in include/{tqr,gridscheduler,gpucalc,qrdecomp}.h; this module only
+binds it (for tests, bench.py and __graft_entry__), mirroring the reference's interface
+(taskQRP_threads / cudaQRTask / SGEQRF ... / the gridscheduler API, reference qrdecomp.h,
+include/gpucalc.h, include/gridscheduler.h). There is no Python or CPU compute path here:
+every factorisation call goes to the HIP kernels, and loading fails loudly if libtqr.so is
+missing.
+
+Array convention: a column-major m x n matrix is a numpy/torch array of shape (n, m)
+(row j = column j), so ldm = m and element (i, j) is A[j, i] — the reference's
+CO(i,j,ldm) = j*ldm + i.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtqr.so")
+
+TQR_F32, TQR_F64 = 0, 1
+QRS, SAPP, QRD, DAPP = 0, 1, 2, 3
+TASK_AVAIL, TASK_NONE, TASK_DONE = 0, 1, 2
+READY, DOING, DONE, NONE, NOTASKS = 0, 1, 2, 3, 4
+
+_lib = None
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+
+
+class TQRError(RuntimeError):
+    pass
+
+
+class Task(ctypes.Structure):
+    """reference include/gridscheduler.h:13-17"""
+    _fields_ = [("taskType", _I), ("l", _I), ("m", _I), ("k", _I), ("taskStatus", _I)]
+
+
+class Plan(ctypes.Structure):
+    """tqr_plan_t, include/gridscheduler.h"""
+    _fields_ = [("M", _I), ("N", _I), ("nlevels", _I), ("ntasks", ctypes.c_long),
+                ("tasks", ctypes.POINTER(_I)), ("level_off", ctypes.POINTER(ctypes.c_long))]
+
+
+def lib():
+    """Load libtqr.so (raises if it was not built: no fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    # PyTorch-ROCm wheels dlopen their own bundled libamdhip64.so.7 by path; if libtqr.so were
+    # loaded first, the process would hold two HIP runtimes and torch would see no GPU. Loading
+    # torch first makes libtqr.so bind (by soname) to the one runtime torch already holds.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise TQRError(f"{LIB_PATH} is missing — build it with __graft_entry__.build() "
+                       "(make -C gpu-tiled-qr-decomposition_amd)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.tqr_strerror.restype = ctypes.c_char_p
+    L.tqr_version.restype = ctypes.c_char_p
+    L.tqr_total_tasks.restype = ctypes.c_long
+    L.tqr_sched_total_tasks.restype = ctypes.c_long
+    L.initScheduler.restype = ctypes.POINTER(Task)
+    L.tqr_plan_create.argtypes = [ctypes.POINTER(_P), _I, _I, _I, _I]
+    L.tqr_plan_execute.argtypes = [_P, _P, _I, _P, _P]
+    L.tqr_plan_destroy.argtypes = [_P]
+    L.tqr_plan_set_profile.argtypes = [_P, _I]
+    L.tqr_plan_stats.argtypes = [_P, ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double)]
+    L.tqr_fill_randzo.argtypes = [_I, _P, _I, _I, _I, ctypes.c_ulonglong, _P]
+    for nm in ("tqr_tile_geqrt", "tqr_tile_unmqr", "tqr_tile_tsqrt", "tqr_tile_tsmqr"):
+        getattr(L, nm).restype = _I
+    L.tqr_dgeqrt_host.argtypes = [_P, _P, _I, _I, _I, _I]
+    L.tqr_sgeqrt_host.argtypes = [_P, _P, _I, _I, _I, _I]
+    _lib = L
+    return L
+
+
+def check(st, what=""):
+    if st != 0:
+        raise TQRError(f"{what}: {lib().tqr_strerror(st).decode()} ({st})")
+
+
+def _ptr(a):
+    if hasattr(a, "data_ptr"):
+        return _P(a.data_ptr())
+    return a.ctypes.data_as(_P)
+
+
+def _dtype_code(dt):
+    dt = np.dtype(dt) if not hasattr(dt, "is_floating_point") else dt
+    if str(dt) in ("float64", "torch.float64"):
+        return TQR_F64
+    if str(dt) in ("float32", "torch.float32"):
+        return TQR_F32
+    raise TQRError(f"unsupported dtype {dt}")
+
+
+# ---- scheduler (host C, no GPU needed) ---------------------------------------------------
+class Scheduler:
+    """The reference gridscheduler API (initScheduler / getNextTask / doneATask)."""
+
+    def __init__(self, M, N):
+        self.M, self.N = M, N
+        self.grid = lib().initScheduler(M, N)
+        if not self.grid:
+            raise TQRError("initScheduler failed")
+
+    def next_task(self):
+        t = Task()
+        r = lib().getNextTask(ctypes.byref(t), self.grid, self.M, self.N)
+        return r, t
+
+    def done(self, t):
+        lib().doneATask(self.grid, self.M, self.N, t)
+
+    def __del__(self):
+        try:
+            ctypes.CDLL(None).free(ctypes.cast(self.grid, _P))
+        except Exception:
+            pass
+
+
+def sched_plan(M, N):
+    """Static wave plan: list of waves, each a list of (type, l, m, k)."""
+    p = Plan()
+    check(lib().tqr_sched_plan(M, N, ctypes.byref(p)), "tqr_sched_plan")
+    tasks = np.ctypeslib.as_array(p.tasks, shape=(p.ntasks * 4,)).reshape(-1, 4).copy()
+    offs = np.ctypeslib.as_array(p.level_off, shape=(p.nlevels + 1,)).copy()
+    lib().tqr_sched_plan_free(ctypes.byref(p))
+    return [tasks[offs[L]:offs[L + 1]] for L in range(len(offs) - 1)]
+
+
+# ---- device factorisation -------------------------------------------------------------------
+class TiledQR:
+    """A planned factorisation (tqr_plan): create once, execute on device arrays."""
+
+    def __init__(self, m, n, b, dtype):
+        self.m, self.n, self.b = m, n, b
+        self.dtype = dtype if isinstance(dtype, int) else _dtype_code(dtype)
+        self.kmax = min(m, n) // b
+        h = _P()
+        check(lib().tqr_plan_create(ctypes.byref(h), m, n, b, self.dtype), "tqr_plan_create")
+        self.h = h
+
+    def execute(self, A, tau, ldda=None, stream=None):
+        """A, tau: device tensors (torch) — A (n, ldda) column-major, tau (kmax, m) compact."""
+        ldda = ldda or self.m
+        check(lib().tqr_plan_execute(self.h, _ptr(A), ldda, _ptr(tau), _P(stream or 0)), "tqr_plan_execute")
+
+    def set_profile(self, on=True):
+        check(lib().tqr_plan_set_profile(self.h, int(on)))
+
+    def stats(self):
+        nu, np_ = _I(), _I()
+        mu, mp = ctypes.c_double(), ctypes.c_double()
+        check(lib().tqr_plan_stats(self.h, ctypes.byref(nu), ctypes.byref(mu), ctypes.byref(np_), ctypes.byref(mp)))
+        return {"n_update": nu.value, "ms_update": mu.value, "n_panel": np_.value, "ms_panel": mp.value}
+
+    def __del__(self):
+        try:
+            lib().tqr_plan_destroy(self.h)
+        except Exception:
+            pass
+
+
+def fill_randzo(A, m, n, seed, ldda=None, stream=None):
+    check(lib().tqr_fill_randzo(_dtype_code(A.dtype), _ptr(A), m, n, ldda or m, seed, _P(stream or 0)),
+          "tqr_fill_randzo")
+
+
+def geqrt_host(A, b):
+    """Factorise a host column-major array (shape (n, m)) in place on the GPU; returns the
+    reference's m x n tau matrix (shape (n, m), zero except columns k*b)."""
+    n, m = A.shape
+    tau = np.zeros_like(A)
+    fn = lib().tqr_dgeqrt_host if A.dtype == np.float64 else lib().tqr_sgeqrt_host
+    check(fn(_ptr(A), _ptr(tau), m, n, m, b), "tqr_geqrt_host")
+    return tau
+
+
+def expand_tau(tau_compact, m, n, b):
+    """compact (kmax, m) -> the reference's m x n tau matrix as an (n, m) array."""
+    T = np.zeros((n, m), dtype=tau_compact.dtype)
+    for k in range(min(m, n) // b):
+        T[k * b, k * b:] = tau_compact[k, k * b:]
+    return T
+
+
+# ---- single tile ops (host pointers; the reference's SGEQRF/SLARFT/STSQRF/SSSRFT) --------
+def _tile_ptr(M, r, c, b):
+    """pointer to tile (r,c) of a column-major matrix stored as (n, m) numpy array"""
+    ldm = M.shape[1]
+    return _P(M.ctypes.data + (c * b * ldm + r * b) * M.itemsize)
+
+
+def tile_geqrt(M, b, tau):
+    check(lib().tqr_tile_geqrt(_dtype_code(M.dtype), _tile_ptr(M, 0, 0, b), _ptr(tau), b, M.shape[1]), "tile_geqrt")
+
+
+def tile_unmqr(M, b, tau):
+    """C = tile (0,1) updated with V, tau of tile (0,0)"""
+    check(lib().tqr_tile_unmqr(_dtype_code(M.dtype), _tile_ptr(M, 0, 1, b), _tile_ptr(M, 0, 0, b), _ptr(tau), b,
+                               M.shape[1]), "tile_unmqr")
+
+
+def tile_tsqrt(M, b, tau):
+    """[R tile (0,0); tile (1,0)]"""
+    check(lib().tqr_tile_tsqrt(_dtype_code(M.dtype), _tile_ptr(M, 0, 0, b), _tile_ptr(M, 1, 0, b), _ptr(tau), b,
+                               M.shape[1]), "tile_tsqrt")
+
+
+def tile_tsmqr(M, b, tau):
+    """V = tile (1,0), A = tile (0,1), B = tile (1,1)"""
+    check(lib().tqr_tile_tsmqr(_dtype_code(M.dtype), _tile_ptr(M, 1, 0, b), _tile_ptr(M, 0, 1, b),
+                               _tile_ptr(M, 1, 1, b), _ptr(tau), b, M.shape[1]), "tile_tsmqr")
+
+
+def flops(m, n):
+    """Algorithmic Householder QR flop count 2mn^2 - 2n^3/3 (m >= n)."""
+    if m >= n:
+        return 2.0 * m * n * n - 2.0 * n ** 3 / 3.0
+    return 2.0 * n * m * m - 2.0 * m ** 3 / 3.0

@@ -1,0 +1,88 @@
+/*
+ * tqr — MI355X-native flat-tree tiled Householder QR (libtqr.so), the native API.
+ *
+ * Same algorithm and output layout as the reference (s10m/GPU-Tiled-QR-Decomposition):
+ *   * A is column-major m x n with leading dimension ldm, factorised in place: the global
+ *     upper triangle is R, the strict lower part of each diagonal tile (k,k) holds the
+ *     unit-lower GEQRT V, and every tile (i,k), i>k, holds the dense TSQRT V_B
+ *     (reference qrdecomp.c:522-523, 683-684);
+ *   * Householder conventions of qrdecomp.c:1201-1272 (sign(0)=+1, v0=1, tau=2/v'v, tau=2
+ *     for length-1 and zero columns).
+ * The tile size b must divide m and n; b in {16, 32, 64, 128, 256}.
+ *
+ * tau, device API: "compact" m x kmax column-major array (kmax = min(m,n)/b), column k holds
+ * the b*(p-k) taus of panel k in rows k*b .. m-1 — exactly column k*b of the reference's
+ * m x n tau matrix (qrdecomp.c:392,420,435). The host API returns the reference's m x n
+ * tau matrix (other entries untouched).
+ *
+ * Status codes: 0 = ok, negative = error (see tqr_strerror).
+ */
+#ifndef TQR_H
+#define TQR_H
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum tqr_status {
+    TQR_OK = 0,
+    TQR_EINVAL = -1,   /* bad sizes / tile size / pointers */
+    TQR_ENOMEM = -2,   /* device or host allocation failed */
+    TQR_EHIP = -3,     /* a HIP runtime call failed */
+    TQR_ENODEV = -4,   /* no usable gfx950 device */
+    TQR_ERCCL = -5     /* an RCCL call failed */
+};
+enum tqr_dtype { TQR_F32 = 0, TQR_F64 = 1 };
+
+const char* tqr_strerror(int status);
+const char* tqr_version(void);
+
+/* ---- plans: allocate once, execute many times (no allocation inside execute) ---------- */
+typedef struct tqr_plan tqr_plan;
+
+/* Plan a factorisation of an m x n matrix of `dtype` with tile size b on the current HIP
+ * device. */
+int tqr_plan_create(tqr_plan** plan, int m, int n, int b, int dtype);
+void tqr_plan_destroy(tqr_plan* plan);
+
+/* Factorise device matrix dA (ldda >= m) in place; dtau_compact is device memory of
+ * m * kmax elements of the same dtype. `stream` is a hipStream_t (NULL = default stream).
+ * Stream-ordered: returns once all work is enqueued. */
+int tqr_plan_execute(tqr_plan* plan, void* dA, int ldda, void* dtau_compact, void* stream);
+
+/* Per-launch statistics of the last execute (filled when the plan was created with
+ * tqr_plan_set_profile(plan, 1)): number of kernel launches and the summed device time of
+ * the trailing-update (TSMQR/UNMQR) and panel (GEQRT/TSQRT) kernels in ms. */
+int tqr_plan_set_profile(tqr_plan* plan, int on);
+int tqr_plan_stats(const tqr_plan* plan, int* nlaunch_update, double* ms_update, int* nlaunch_panel,
+                   double* ms_panel);
+
+/* Number of flat-tree tasks (reference calcTotalTasks, src/gpucalc.cu:1546, for all m,n). */
+long tqr_total_tasks(int m, int n, int b);
+
+/* ---- one-shot helpers ------------------------------------------------------------------ */
+/* Device pointers, stream-ordered; plan cached per (m,n,b,dtype). */
+int tqr_dgeqrt_tiled(int m, int n, int b, double* dA, int ldda, double* dtau_compact, void* stream);
+int tqr_sgeqrt_tiled(int m, int n, int b, float* dA, int ldda, float* dtau_compact, void* stream);
+
+/* Host pointers, blocking: A in place; tau = the reference's m x n tau matrix (ldm). */
+int tqr_dgeqrt_host(double* A, double* tau, int m, int n, int ldm, int b);
+int tqr_sgeqrt_host(float* A, float* tau, int m, int n, int ldm, int b);
+
+/* Host pointers, single tile tasks on the GPU (the reference's per-tile kernels; used by
+ * qrdecomp.h's SGEQRF/SLARFT/STSQRF/SSSRFT and by the per-tile parity tests). Tile pointers
+ * are tile origins inside one ldm-strided matrix; tau pointers point at the tile's b
+ * consecutive taus, as in the reference. */
+int tqr_tile_geqrt(int dtype, void* blk, void* tau, int b, int ldm);
+int tqr_tile_unmqr(int dtype, void* C, const void* V, const void* tau, int b, int ldm);
+int tqr_tile_tsqrt(int dtype, void* A, void* B, void* tau, int b, int ldm);
+int tqr_tile_tsmqr(int dtype, const void* V, void* A, void* B, const void* tau, int b, int ldm);
+
+/* Device-side synthetic input with the reference's RANDZO distribution
+ * ((r mod 201) - 100)/100 (qrdecomp.c:1383), from a counter-based hash of (seed, i, j). */
+int tqr_fill_randzo(int dtype, void* dA, int m, int n, int ldda, unsigned long long seed, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

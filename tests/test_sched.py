@@ -1,0 +1,74 @@
+"""The product scheduler (csrc/sched.c) against the reference scheduler's own behaviour."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+
+def test_trace_matches_reference(tqr):
+    g = golden("sched.npz")
+    for key in g.files:
+        if not key.startswith("trace_"):
+            continue
+        M, N = map(int, key.split("_")[1].split("x"))
+        s = tqr.Scheduler(M, N)
+        out = []
+        while True:
+            r, t = s.next_task()
+            if r != tqr.TASK_AVAIL:
+                assert r == tqr.TASK_DONE
+                break
+            out.append((t.taskType, t.l, t.m, t.k))
+            s.done(t)
+        assert np.array_equal(np.array(out, dtype=np.int32).reshape(-1, 4), g[key]), key
+
+
+def test_waves_match_reference(tqr):
+    g = golden("sched.npz")
+    for key in g.files:
+        if not key.startswith("levels_"):
+            continue
+        M, N = map(int, key.split("_")[1].split("x"))
+        waves = tqr.sched_plan(M, N)
+        assert np.array_equal(np.array([len(w) for w in waves]), g[key]), key
+
+
+@pytest.mark.parametrize("M,N", [(1, 1), (5, 3), (3, 5), (7, 7), (64, 64), (256, 64)])
+def test_plan_is_topological(tqr, M, N):
+    """Every dependency of a task sits in an earlier wave; every task appears once; inside a
+    wave no two tasks write the same tile."""
+    waves = tqr.sched_plan(M, N)
+    wave_of = {}
+    for L, w in enumerate(waves):
+        for (ty, l, m, k) in w:
+            assert (l, m, k) not in wave_of
+            wave_of[(l, m, k)] = L
+    assert len(wave_of) == tqr.lib().tqr_sched_total_tasks(M, N)
+    for (l, m, k), L in wave_of.items():
+        deps = []
+        if k > 0:
+            deps.append((l, m, k - 1))
+        if l == k and m > k:
+            deps.append((k, k, k))
+        if l > k and m == k:
+            deps.append((l - 1, k, k))
+        if l > k and m > k:
+            deps += [(l, k, k), (l - 1, m, k)]
+        for d in deps:
+            assert wave_of[d] < L
+        if M * N <= 49:
+            continue
+    for w in waves:  # writes inside a wave are disjoint
+        written = set()
+        for (ty, l, m, k) in w:
+            tiles = {(l, m)} | ({(k, m)} if ty == tqr.DAPP else set()) | ({(k, k)} if ty == tqr.QRD else set())
+            assert not (tiles & written)
+            written |= tiles
+
+
+def test_total_tasks(tqr):
+    assert tqr.lib().tqr_sched_total_tasks(64, 64) == 89440
+    assert tqr.lib().tqr_sched_total_tasks(256, 64) == 488800
+    assert tqr.lib().tqr_sched_total_tasks(3, 6) == 32  # the reference's calcTotalTasks says 28
+    assert tqr.lib().tqr_total_tasks(16384, 16384, 256) == 89440
+    assert tqr.lib().tqr_total_tasks(100, 64, 32) == -1
