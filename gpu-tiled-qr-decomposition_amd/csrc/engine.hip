@@ -40,6 +40,24 @@ struct Args {
   int m, p, kmax;
 };
 
+#ifdef TQR_STAMPS
+// Diagnostic build only (make stamps): per-phase cycle sums of the panel kernel's TSQRT tasks.
+__device__ unsigned long long g_stamps[8];
+__device__ unsigned long long g_pstamps[8];
+#define STAMP_INIT unsigned long long st_last = __builtin_amdgcn_s_memrealtime();
+#define STAMP(i)                                                          \
+  do {                                                                    \
+    if (threadIdx.x == 0) {                                               \
+      unsigned long long now_ = __builtin_amdgcn_s_memrealtime();             \
+      atomicAdd(&g_stamps[i], now_ - st_last);                            \
+      st_last = now_;                                                     \
+    }                                                                     \
+  } while (0)
+#else
+#define STAMP_INIT
+#define STAMP(i) do {} while (0)
+#endif
+
 template <int B>
 __device__ __forceinline__ double* tw_ptr(const Args& a, int i, int k, int g) {
   using G = Geo<B>;
@@ -60,6 +78,7 @@ __global__ __launch_bounds__(NT, 1) void k_panel(Args a) {
   double* Gs = Ts + G::TSZ;
   double* tauv = Gs + G::TSZ;
   double* scratch = tauv + IB + 2;
+  double* Gp = scratch + 2 * 4 * 32 + 4 * 32 + 2 * 32 + G::TSZ;  // 4 partial Grams
 
   const Item it = a.items[blockIdx.x];
   const int type = it.ts & 0xff, l = it.l, k = it.k;
@@ -74,6 +93,7 @@ __global__ __launch_bounds__(NT, 1) void k_panel(Args a) {
   if (type == QRS) {
     for (int g = 0; g < NG; ++g) {
       const int c0 = g * IB, ks0 = c0 / 4;
+#pragma unroll 8
       for (int idx = t; idx < B * IB; idx += NT) {
         int r = idx % B, c = idx / B;
         Vs[r * VP + G::pc(c)] = r >= c0 ? ld(Rt + (size_t)(c0 + c) * ldm + r) : 0.0;
@@ -93,12 +113,13 @@ __global__ __launch_bounds__(NT, 1) void k_panel(Args a) {
         if (r <= d) Vs[r * VP + G::pc(c)] = r == d ? 1.0 : 0.0;
       }
       __syncthreads();
-      build_t<B>(Vs, tauv, Gs, Ts, ks0);
+      build_t<B>(Vs, tauv, Gs, Ts, Gp, ks0);
       double* tg = tw_ptr<B>(a, k, k, g);
       for (int idx = t; idx < IB * IB; idx += NT) tg[idx] = Ts[(idx / IB) * TP + idx % IB];
       // trailing columns of the tile
       const int nstr = (B - c0 - IB) / 16;
       for (int s = w; s < nstr; s += NT / 64) {
+        asm volatile("" ::: "memory");  // keep the V-image reads inside the loop (no LICM of ~1k LDS loads)
         const int col = c0 + IB + 16 * s;
         load_strip<B>(X, Rt, ldm, col, ks0);
         apply_group<B, false>(Vs, Ts, X, H, ks0);
@@ -108,8 +129,10 @@ __global__ __launch_bounds__(NT, 1) void k_panel(Args a) {
     }
   } else {  // QRD: TSQRT of [R_kk ; tile (l,k)]
     S* Bt = A + (size_t)k * B * ldm + (size_t)l * B;
+    STAMP_INIT
     for (int g = 0; g < NG; ++g) {
       const int c0 = g * IB;
+#pragma unroll 8
       for (int idx = t; idx < B * IB; idx += NT) {
         int r = idx % B, c = idx / B;
         Vs[r * VP + G::pc(c)] = ld(Bt + (size_t)(c0 + c) * ldm + r);
@@ -119,7 +142,9 @@ __global__ __launch_bounds__(NT, 1) void k_panel(Args a) {
         if (r <= c) Hs[r * TP + c] = ld(Rt + (size_t)(c0 + c) * ldm + c0 + r);
       }
       __syncthreads();
+      STAMP(0);
       panel_factor<B, true>(Vs, Hs, tauv, scratch, c0);
+      STAMP(1);
       for (int idx = t; idx < B * IB; idx += NT) {
         int r = idx % B, c = idx / B;
         st(Bt + (size_t)(c0 + c) * ldm + r, Vs[r * VP + G::pc(c)]);
@@ -130,11 +155,14 @@ __global__ __launch_bounds__(NT, 1) void k_panel(Args a) {
       }
       if (t < IB) st(tau + (size_t)k * a.m + (size_t)l * B + c0 + t, tauv[t]);
       __syncthreads();
-      build_t<B>(Vs, tauv, Gs, Ts, 0);
+      STAMP(2);
+      build_t<B>(Vs, tauv, Gs, Ts, Gp, 0);
+      STAMP(3);
       double* tg = tw_ptr<B>(a, l, k, g);
       for (int idx = t; idx < IB * IB; idx += NT) tg[idx] = Ts[(idx / IB) * TP + idx % IB];
       const int nstr = (B - c0 - IB) / 16;
       for (int s = w; s < nstr; s += NT / 64) {
+        asm volatile("" ::: "memory");  // keep the V-image reads inside the loop (no LICM of ~1k LDS loads)
         const int col = c0 + IB + 16 * s;
         load_strip<B>(X, Bt, ldm, col, 0);
         load_head<B>(H, Rt, ldm, c0, col);
@@ -143,6 +171,7 @@ __global__ __launch_bounds__(NT, 1) void k_panel(Args a) {
         store_head<B>(H, Rt, ldm, c0, col);
       }
       __syncthreads();
+      STAMP(4);
     }
   }
 }
@@ -212,6 +241,7 @@ __global__ __launch_bounds__(NT, 1) void k_build_t(Args a) {
   double* Ts = Vs + G::VSZ;
   double* Gs = Ts + G::TSZ;
   double* tauv = Gs + G::TSZ;
+  double* Gp = tauv + IB + 2;
   const Item it = a.items[blockIdx.x / NG];
   const int g = blockIdx.x % NG, c0 = g * IB, type = it.ts & 0xff, l = it.l, k = it.k;
   const S* A = (const S*)a.A;
@@ -222,7 +252,7 @@ __global__ __launch_bounds__(NT, 1) void k_build_t(Args a) {
   else stage_v_ts<B>(Vs, A + (size_t)k * B * ldm + (size_t)l * B, ldm, c0);
   if (threadIdx.x < IB) tauv[threadIdx.x] = ld(tau + (size_t)k * a.m + row0 + c0 + threadIdx.x);
   __syncthreads();
-  build_t<B>(Vs, tauv, Gs, Ts, type == QRS ? c0 / 4 : 0);
+  build_t<B>(Vs, tauv, Gs, Ts, Gp, type == QRS ? c0 / 4 : 0);
   double* tg = tw_ptr<B>(a, type == QRS ? k : l, k, g);
   for (int idx = threadIdx.x; idx < IB * IB; idx += NT) tg[idx] = Ts[(idx / IB) * TP + idx % IB];
 }
@@ -246,7 +276,7 @@ __global__ void k_randzo(S* A, int m, int n, long ldm, unsigned long long seed) 
 // ---------------------------------------------------------------------------------------
 static size_t lds_panel(int b) {
   int ib = b < 32 ? b : 32;
-  size_t d = (size_t)b * (ib + 2) + 3 * (size_t)ib * (ib + 1) + (ib + 2) + 8 * 33 + 2 * (ib + 1) + 4;
+  size_t d = (size_t)b * (ib + 2) + 8 * (size_t)ib * (ib + 1) + (ib + 2) + 2 * 4 * 32 + 4 * 32 + 2 * 32;
   return d * sizeof(double);
 }
 static size_t lds_update(int b) {
@@ -263,7 +293,7 @@ static void get_kernels(kfn* p, kfn* u, kfn* t) {
 }
 static size_t lds_build_t(int b) {
   int ib = b < 32 ? b : 32;
-  return ((size_t)b * (ib + 2) + 2 * (size_t)ib * (ib + 1) + ib + 2) * sizeof(double);
+  return ((size_t)b * (ib + 2) + 6 * (size_t)ib * (ib + 1) + ib + 2) * sizeof(double);
 }
 // Resolve the kernels of one (b, dtype) and raise their dynamic-LDS limits.
 static int resolve(int b, int dtype, kfn* kp, kfn* ku, kfn* kt) {
@@ -699,3 +729,16 @@ int tqr_tile_tsmqr(int dtype, const void* V, void* A, void* Bm, const void* tau,
 }
 
 }  // extern "C"
+
+#ifdef TQR_STAMPS
+extern "C" int tqr_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return TQR_EHIP;
+  if (hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(g_pstamps), sizeof(unsigned long long) * 8) != hipSuccess) return TQR_EHIP;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess) return TQR_EHIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pstamps), z, sizeof z) != hipSuccess) return TQR_EHIP;
+  }
+  return TQR_OK;
+}
+#endif

@@ -7,7 +7,7 @@
 //   * a reflector group g (IB consecutive reflectors of a tile) is applied to a column strip
 //     X as   Z = [head] + V_g^T X ;  W = T_g^T Z ;  [head] -= W ;  X -= V_g W
 //     with the three products on v_mfma_f64_4x4x4_4b_f64 (measured ~1.5x the issue rate of
-//     v_mfma_f64_16x16x4_f64 on gfx950, profiles/r01_ubench_mfma.txt);
+//     v_mfma_f64_16x16x4_f64 on gfx950, profiles/r01/ubench_mfma_f64.txt);
 //   * the IB-column panel of GEQRT/TSQRT is factorised in LDS, reflector by reflector, with
 //     the reference's conventions (qrdecomp.c:1201-1272): sign(0) = +1, v scaled to v0 = 1
 //     by the reciprocal of x0 + sign*|x|, no scaling for a zero column, tau = 2/(v'v);
@@ -17,7 +17,7 @@
 // Mathematically every tile op applies exactly the reflectors the reference applies, in the
 // same order; only the rounding differs (parity tolerances in tests/).
 //
-// Register layout of a 4x4x4_4b operand (probed, profiles/r01_ubench_mfma_probe.txt):
+// Register layout of a 4x4x4_4b operand (probed, profiles/r01/ubench_mfma_probe.txt):
 // lane = 16*x + 4*blk + y holds A[blk][i=y][k=x], B[blk][k=x][j=y], D[blk][i=x][j=y].
 // A wave owns a strip of 16 matrix columns (blk = column quad, y = column in quad); register
 // X[ks] holds rows 4ks..4ks+3 of the strip (row 4ks+x at lane x), which is at the same time
@@ -27,6 +27,22 @@
 #include <hip/hip_runtime.h>
 
 namespace tqr {
+
+#ifdef TQR_STAMPS
+extern __device__ unsigned long long g_pstamps[8];
+#define PSTAMP(i)                                                  \
+  do {                                                             \
+    if (threadIdx.x == 0) {                                        \
+      unsigned long long n_ = __builtin_amdgcn_s_memtime();        \
+      atomicAdd(&g_pstamps[i], n_ - ps_last);                      \
+      ps_last = n_;                                                \
+    }                                                              \
+  } while (0)
+#define PSTAMP_INIT unsigned long long ps_last = __builtin_amdgcn_s_memtime();
+#else
+#define PSTAMP(i) do {} while (0)
+#define PSTAMP_INIT
+#endif
 
 constexpr int NT = 256;  // threads per workgroup (4 waves)
 
@@ -178,6 +194,7 @@ __device__ __forceinline__ void store_head(const double (&H)[Geo<B>::NRI], S* __
 template <int B, typename S>
 __device__ __forceinline__ void stage_v_ts(double* Vs, const S* __restrict__ vt, size_t ldm, int c0) {
   using g = Geo<B>;
+#pragma unroll 8
   for (int idx = threadIdx.x; idx < B * g::IB; idx += NT) {
     int r = idx % B, c = idx / B;
     Vs[r * g::VP + g::pc(c)] = ld(vt + (size_t)(c0 + c) * ldm + r);
@@ -187,6 +204,7 @@ __device__ __forceinline__ void stage_v_ts(double* Vs, const S* __restrict__ vt,
 template <int B, typename S>
 __device__ __forceinline__ void stage_v_ge(double* Vs, const S* __restrict__ vt, size_t ldm, int c0) {
   using g = Geo<B>;
+#pragma unroll 8
   for (int idx = threadIdx.x; idx < B * g::IB; idx += NT) {
     int r = idx % B, c = idx / B, d = c0 + c;
     Vs[r * g::VP + g::pc(c)] = r < d ? 0.0 : (r == d ? 1.0 : ld(vt + (size_t)d * ldm + r));
@@ -202,119 +220,318 @@ __device__ __forceinline__ void stage_t(double* Ts, const double* __restrict__ t
 }
 
 // ---------------------------------------------------------------------------------------
-// Panel factorisation of reflector group g in LDS (all NT threads).
-// GE (GEQRT): Vs holds tile rows 0..B-1 of the IB panel columns (rows < c0 unused).
-// TS (TSQRT): Hs holds the IB x IB head block R[c0.., c0..] (upper part used), Vs the B x IB
-// block of the tile below. On exit: R entries in place, V (unit diag implied) in place,
-// tauv[c] = tau of reflector c. scratch: >= 8*33 + 2*(IB+1) + 4 doubles.
+// Wave-level reduce-scatter of N (power of two, <= 32) per-lane values: on return lane l holds
+// the sum over the 64 lanes of value index  (l >> (6 - log2 N)) & (N - 1)... see rs_col().
+// Cost: N - 1 + (6 - log2 N) shuffles instead of 6N for N independent butterflies.
 // ---------------------------------------------------------------------------------------
+// Cross-lane exchange primitives (VALU, no LDS): v_permlane32_swap / v_permlane16_swap and
+// DPP row_mirror / row_half_mirror / quad_perm.
+__device__ __forceinline__ double dbl_of(unsigned lo, unsigned hi) {
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// a[32..63] <-> b[0..31]  (per 32-bit half)
+__device__ __forceinline__ void swap32(double& a, double& b) {
+  const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
+  const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
+  auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+  auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+  a = dbl_of(lo[0], hi[0]);
+  b = dbl_of(lo[1], hi[1]);
+}
+// odd 16-lane rows of a <-> even rows of b
+__device__ __forceinline__ void swap16(double& a, double& b) {
+  const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
+  const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
+  auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ua, (unsigned)ub, false, false);
+  auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+  a = dbl_of(lo[0], hi[0]);
+  b = dbl_of(lo[1], hi[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  return __builtin_amdgcn_update_dpp(0.0, v, CTRL, 0xf, 0xf, false);
+}
+constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_QUAD_3210 = 0x1B, DPP_QUAD_1032 = 0xB1;
+
+// One halving stage on lane-pairs given by a DPP mirror: lanes with `up` keep the upper half.
+template <int CTRL, int H>
+__device__ __forceinline__ void dpp_halve(const double* v, double* out, bool up) {
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    const double send = up ? v[i] : v[i + H];
+    const double keep = up ? v[i + H] : v[i];
+    out[i] = keep + dpp<CTRL>(send);
+  }
+}
+
+// Reduce-scatter of N = 32 or 16 per-lane doubles over the wave: on return lane l holds the
+// wave sum of value index rs_col<N>(l). Stages pair lanes l^32 and l^16 with permlane swaps
+// (no selects), then mirror partners inside 16-, 8- and 4-lane groups by DPP.
+template <int N>
+struct RS {
+  __device__ static __forceinline__ double run(double (&v)[N], int lane) {
+    static_assert(N == 32 || N == 16, "IB must be 16 or 32");
+    constexpr int H1 = N / 2, H2 = N / 4, H3 = N / 8;
+#pragma unroll
+    for (int i = 0; i < H1; ++i) {
+      double a = v[i], b = v[i + H1];
+      swap32(a, b);
+      v[i] = a + b;  // lanes < 32: index i, lanes >= 32: index i + H1
+    }
+#pragma unroll
+    for (int i = 0; i < H2; ++i) {
+      double a = v[i], b = v[i + H2];
+      swap16(a, b);
+      v[i] = a + b;
+    }
+    double c[H3 > 0 ? H3 : 1];
+    dpp_halve<DPP_ROW_MIRROR, H3>(v, c, lane & 8);
+    double e;
+    if constexpr (N == 32) {
+      double d2[2];
+      dpp_halve<DPP_ROW_HALF_MIRROR, 2>(c, d2, lane & 4);
+      double d1[1];
+      dpp_halve<DPP_QUAD_3210, 1>(d2, d1, lane & 2);
+      e = d1[0];
+    } else {
+      double d1[1];
+      dpp_halve<DPP_ROW_HALF_MIRROR, 1>(c, d1, lane & 4);
+      e = d1[0];
+      e += dpp<DPP_QUAD_3210>(e);
+    }
+    e += dpp<DPP_QUAD_1032>(e);
+    return e;
+  }
+};
+template <int N>
+__device__ __forceinline__ int rs_col(int lane) {
+  // bit for xor 32 is the top index bit, then xor 16, ...
+  int c = 0;
+#pragma unroll
+  for (int k = 0, X = 32; (1 << k) < N; ++k, X >>= 1) c = (c << 1) | ((lane & X) ? 1 : 0);
+  return c;
+}
+
+// ---------------------------------------------------------------------------------------
+// Panel factorisation of reflector group g (all NT threads; row-per-thread registers).
+// On entry Vs holds the panel's B tile rows (perm layout; GE: rows >= c0 used), and for TS
+// Hs holds the IB x IB head block R[c0.., c0..] (upper part used). Thread t owns panel row t.
+// Per reflector c ONE workgroup reduction gives the raw dots D_j = x_c . x_j (tail rows,
+// j >= c); D_c is the squared tail norm, so
+//   norm = sqrt(x0^2 + D_c), v = x_c / (x0 + sign(x0) norm)  [no scaling if norm == 0],
+//   tau = 2 / (1 + |v|^2),  d_j = head_j + v . x_j,  x_j -= tau d_j v,  head_j -= tau d_j
+// — the reference's reflector (qrdecomp.c:1201-1272, 647-687) with its sums regrouped.
+// On exit: Vs rows hold R (GE head rows) / V (tails) in place, Hs (TS) the updated head block,
+// tauv[c] = tau_c. scratch >= 2*4*32 + 4*32 + 2*32 + IB*TP doubles.
+// ---------------------------------------------------------------------------------------
+// 1/a to full double precision: v_rcp_f64 + two Newton steps (a != 0, finite).
+__device__ __forceinline__ double rcp_nr(double a) {
+  double r = __builtin_amdgcn_rcp(a);
+  r = fma(fma(-a, r, 1.0), r, r);
+  r = fma(fma(-a, r, 1.0), r, r);
+  return r;
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+  return dbl_of(lo, hi);
+}
+
+// One reflector step; C is a template parameter so x[C] and the j-windows are static (a
+// runtime c would force x[] into scratch memory).
+//   1. every tail row forms x_C * x_j (j in the live window) and the wave reduce-scatters them;
+//   2. one barrier; each lane sums the 4 wave partials of "its" column j and reads head_j;
+//   3. the pivot's D_C and head_C are read from the owning lane (s_readlane, uniform);
+//   4. lane of column j forms f_j = tau (head_j + scale D_j) and publishes it wave-privately;
+//   5. rows update x_j -= f_j v (tails) / head_j -= f_j (GE head row, TS head in `hout`).
+template <int B, bool TS, int C>
+__device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Hs, double* tauv, double* red, double* wb,
+                                           double* hrow, double* hout, int c0, bool own, int mycol, bool writer) {
+  using g = Geo<B>;
+  constexpr int IB = g::IB, TP = g::TP;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int rc = c0 + C;  // GE: tile row of the reflector head
+  const bool tail = own && (TS || t > rc);
+  PSTAMP_INIT
+  // reduce only the live window j >= C: 32 wide, or the upper 16 once C >= 16
+  constexpr int NW = (IB == 32 && C >= 16) ? 16 : IB;
+  constexpr int J0 = IB - NW;
+  constexpr int SPAN = 64 / NW;          // lanes holding the same column after reduce-scatter
+  constexpr int LC = (C - J0) * SPAN;    // a lane holding column C (rs_col is lane / SPAN)
+  double pv[NW];
+#pragma unroll
+  for (int j = 0; j < NW; ++j) pv[j] = (J0 + j >= C && tail) ? x[C] * x[J0 + j] : 0.0;
+  const double ws = RS<NW>::run(pv, lane);
+  const int cw = J0 + rs_col<NW>(lane);
+  const bool wr = (lane & (SPAN - 1)) == 0;
+  double* rb = red + (C & 1) * 128;
+  if (wr) rb[w * 32 + cw] = ws;
+  if (!TS && t == rc) {
+#pragma unroll
+    for (int j = C; j < IB; ++j) hrow[(C & 1) * 32 + j] = x[j];
+  }
+  PSTAMP(0);
+  __syncthreads();
+  PSTAMP(1);
+  const double* Hh = TS ? (Hs + C * TP) : (hrow + (C & 1) * 32);
+  const double Dm = (rb[cw] + rb[32 + cw]) + (rb[64 + cw] + rb[96 + cw]);
+  const double Hm = Hh[cw];
+  const double dc = readlane_d(Dm, LC);
+  const double x0 = readlane_d(Hm, LC);
+  const double norm = sqrt(x0 * x0 + dc);
+  const double hd = x0 + (x0 >= 0.0 ? norm : -norm);
+  const double scale = norm != 0.0 ? rcp_nr(hd) : 1.0;
+  const double tau = 2.0 * rcp_nr(fma(scale * scale, dc, 1.0));
+  const double fm = tau * fma(scale, Dm, Hm);  // f_j for j = cw
+  double* fb = wb + w * 32;
+  if (wr) fb[cw] = fm;
+  if (TS && w == 0 && wr && cw >= C) hout[C * TP + cw] = Hm - fm;  // cw == C: R_CC = x0 - f_C
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  double f[NW];
+#pragma unroll
+  for (int h = 0; h < NW / 2; ++h) {
+    const double2 v2 = reinterpret_cast<const double2*>(fb + J0)[h];
+    f[2 * h] = v2.x;
+    f[2 * h + 1] = v2.y;
+  }
+  PSTAMP(2);
+  if (tail) {
+    const double xc = x[C] * scale;
+#pragma unroll
+    for (int j = C + 1; j < IB; ++j) x[j] = fma(-f[j - J0], xc, x[j]);
+    x[C] = xc;
+  } else if (!TS && t == rc) {
+#pragma unroll
+    for (int j = C + 1; j < IB; ++j) x[j] -= f[j - J0];
+    x[C] = x0 - f[C - J0];
+  }
+  if (t == 0) tauv[C] = tau;
+  PSTAMP(3);
+}
+
+template <int B, bool TS, int C>
+struct PanelSteps {
+  __device__ static __forceinline__ void run(double (&x)[Geo<B>::IB], double* Hs, double* tauv, double* red, double* wb,
+                                             double* hrow, double* hout, int c0, bool own, int mycol, bool writer) {
+    if constexpr (C < Geo<B>::IB) {
+      panel_step<B, TS, C>(x, Hs, tauv, red, wb, hrow, hout, c0, own, mycol, writer);
+      PanelSteps<B, TS, C + 1>::run(x, Hs, tauv, red, wb, hrow, hout, c0, own, mycol, writer);
+    }
+  }
+};
+
 template <int B, bool TS>
 __device__ void panel_factor(double* Vs, double* Hs, double* tauv, double* scratch, int c0) {
   using g = Geo<B>;
   constexpr int IB = g::IB, VP = g::VP, TP = g::TP;
-  double* red2 = scratch;             // 8 x 33 partial dots
-  double* dsum = scratch + 8 * 33;    // IB + 1: full dots d_j, dsum[IB] = tail dot of the pivot
-  double* red = dsum + 2 * (IB + 1);  // 4
-  const int t = threadIdx.x, jj = t & 31, ch = t >> 5;
-  for (int c = 0; c < IB; ++c) {
-    const int rc = TS ? -1 : c0 + c;  // GE: tile row of the reflector head; tail rows > rc
-    const int pcc = g::pc(c);
-    const double x0 = TS ? Hs[c * TP + c] : Vs[rc * VP + pcc];
-    double xr = (t > rc && t < B) ? Vs[t * VP + pcc] : 0.0;
-    const double s = block_sum(xr * xr, red);
-    const double norm = sqrt(x0 * x0 + s);
-    const double hd = x0 + (x0 >= 0.0 ? norm : -norm);
-    const double scale = norm != 0.0 ? 1.0 / hd : 1.0;
-    // partial dots of the tail rows with the (scaled) reflector, columns c..IB-1
-    double part = 0.0;
-    if (jj >= c && jj < IB) {
-      const int pj = g::pc(jj);
-      for (int r = rc + 1 + ch; r < B; r += 8) part += Vs[r * VP + pj] * (Vs[r * VP + pcc] * scale);
-    }
-    red2[ch * 33 + jj] = part;
-    __syncthreads();
-    if (t >= c && t < IB) {
-      double d = 0.0;
+  double* red = scratch;             // 2 x [4 waves][32] cross-wave partials (double-buffered)
+  double* wb = red + 2 * 4 * 32;     // [4 waves][32] per-wave totals
+  double* hrow = wb + 4 * 32;        // 2 x [32] GE head row broadcast (double-buffered)
+  double* hout = hrow + 2 * 32;      // [IB][TP] TS updated head rows
+  const int t = threadIdx.x, lane = t & 63;
+  const bool own = t < B && (TS || t >= c0);
+  double x[IB];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) d += red2[q * 33 + t];
-      const double head = TS ? Hs[c * TP + t] : Vs[rc * VP + g::pc(t)];
-      dsum[t] = head + d;
-      if (t == c) dsum[IB] = d;
-    }
-    __syncthreads();
-    const double tau = 2.0 / (1.0 + scale * dsum[IB]);
-    if (jj > c && jj < IB) {
-      const int pj = g::pc(jj);
-      const double f = tau * dsum[jj];
-      for (int r = rc + 1 + ch; r < B; r += 8) Vs[r * VP + pj] -= f * (Vs[r * VP + pcc] * scale);
-      if (ch == 0) {
-        if (TS) Hs[c * TP + jj] -= f;
-        else Vs[rc * VP + pj] -= f;
-      }
-    }
-    __syncthreads();
-    if (t > rc && t < B) Vs[t * VP + pcc] *= scale;
-    if (t == 0) {
-      const double rcc = x0 - tau * dsum[c];
-      if (TS) Hs[c * TP + c] = rcc;
-      else Vs[rc * VP + pcc] = rcc;
-      tauv[c] = tau;
+  for (int j = 0; j < IB; ++j) x[j] = own ? Vs[t * VP + g::pc(j)] : 0.0;
+  const int mycol = rs_col<IB>(lane);
+  const bool writer = (lane & (64 / IB - 1)) == 0;
+  PanelSteps<B, TS, 0>::run(x, Hs, tauv, red, wb, hrow, hout, c0, own, mycol, writer);
+  if (own) {
+#pragma unroll
+    for (int j = 0; j < IB; ++j) Vs[t * VP + g::pc(j)] = x[j];
+  }
+  __syncthreads();
+  if (TS) {
+    for (int idx = t; idx < IB * IB; idx += NT) {
+      const int r = idx / IB, c = idx % IB;
+      if (r <= c) Hs[r * TP + c] = hout[r * TP + c];
     }
     __syncthreads();
   }
 }
 
 // ---------------------------------------------------------------------------------------
-// T_g from the explicit V image and tauv: Gram G = V^T V on MFMA (waves 0..IB/16-1), then
-// T[c][c] = tau_c, T[0:c,c] = -tau_c T[0:c,0:c] G[0:c,c] column by column.
+// T_g from the explicit V image and tauv.
+//  1. Gram G = V^T V on MFMA, the B tile rows split over the 4 waves (64 rows each), partial
+//     Grams summed in a fixed order (Gp: 4 x IB x TP scratch).
+//  2. T = U^{-1} with U = diag(1/tau) + strict_upper(G) (the compact-WY identity
+//     T^{-1} + T^{-T} = V^T V; this is LAPACK dlarft's forward columnwise T): 32 columns
+//     solved in parallel by back substitution, 8 lanes per column, DPP-reduced dot products.
 // Gs, Ts: IB x TP images. ks0: first non-zero 4-row block of V (GE), 0 for TS.
 // ---------------------------------------------------------------------------------------
 template <int B>
-__device__ void build_t(const double* Vs, const double* tauv, double* Gs, double* Ts, int ks0) {
+__device__ void build_t(const double* Vs, const double* tauv, double* Gs, double* Ts, double* Gp, int ks0) {
   using g = Geo<B>;
   constexpr int IB = g::IB, VP = g::VP, TP = g::TP, NKS = g::NKS, NRI = g::NRI;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3, blk = (lane >> 2) & 3;
-  if (w < (IB + 15) / 16) {
-    const int cb = 16 * w + 4 * blk + y;  // Gram column of this lane's B operand
-    double Z[NRI];
+  constexpr int KPW = (NKS + 3) / 4;  // k-steps per wave
+  constexpr int NCH = IB / 16;        // 16-column halves of the Gram
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63, x = lane >> 4, y = lane & 3, blk = (lane >> 2) & 3;
+  {
+    double Z[NCH][NRI];
 #pragma unroll
-    for (int r = 0; r < NRI; ++r) Z[r] = 0.0;
-    if (cb < IB) {
+    for (int h = 0; h < NCH; ++h)
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        if (ks < ks0) continue;
-        const double xb = Vs[(4 * ks + x) * VP + g::pc(cb)];
-        const double2* vr = reinterpret_cast<const double2*>(Vs + (4 * ks + x) * VP + y * NRI);
-        double a[NRI];
+      for (int r = 0; r < NRI; ++r) Z[h][r] = 0.0;
 #pragma unroll
-        for (int h = 0; h < NRI / 2; ++h) {
-          double2 tt = vr[h];
-          a[2 * h] = tt.x;
-          a[2 * h + 1] = tt.y;
-        }
+    for (int kk = 0; kk < KPW; ++kk) {
+      const int ks = w * KPW + kk;
+      if (ks >= NKS || ks < ks0) continue;
+      const double2* vr = reinterpret_cast<const double2*>(Vs + (4 * ks + x) * VP + y * NRI);
+      double a[NRI];
 #pragma unroll
-        for (int r = 0; r < NRI; ++r) Z[r] = mfma4(a[r], xb, Z[r]);
+      for (int q = 0; q < NRI / 2; ++q) {
+        double2 tt = vr[q];
+        a[2 * q] = tt.x;
+        a[2 * q + 1] = tt.y;
       }
-    } else {
-      // IB = 16 with 16 Gram columns per wave: no idle lanes; kept for generality.
-    }
-    if (cb < IB) {
 #pragma unroll
-      for (int r = 0; r < NRI; ++r) Gs[(4 * r + x) * TP + cb] = Z[r];
+      for (int h = 0; h < NCH; ++h) {
+        const double xb = Vs[(4 * ks + x) * VP + g::pc(16 * h + 4 * blk + y)];
+#pragma unroll
+        for (int r = 0; r < NRI; ++r) Z[h][r] = mfma4(a[r], xb, Z[h][r]);
+      }
+    }
+    double* gp = Gp + w * IB * TP;
+#pragma unroll
+    for (int h = 0; h < NCH; ++h)
+#pragma unroll
+      for (int r = 0; r < NRI; ++r) gp[(4 * r + x) * TP + 16 * h + 4 * blk + y] = Z[h][r];
+  }
+  __syncthreads();
+  for (int idx = t; idx < IB * IB; idx += NT) {
+    const int r = idx / IB, c = idx % IB, o = r * TP + c;
+    Gs[o] = (Gp[o] + Gp[IB * TP + o]) + (Gp[2 * IB * TP + o] + Gp[3 * IB * TP + o]);
+  }
+  __syncthreads();
+  // back substitution: column j = t >> 3 (t < 8*IB), lane e = t & 7 holds x_k, k = e + 8q
+  constexpr int NQ = IB / 8;
+  const int j = t >> 3, e = t & 7;
+  if (j < IB) {
+    double xr[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) xr[q] = (e + 8 * q == j) ? tauv[j] : 0.0;
+#pragma unroll
+    for (int i = IB - 2; i >= 0; --i) {
+      double part = 0.0;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int k = e + 8 * q;
+        part += (k > i && k <= j) ? Gs[i * TP + k] * xr[q] : 0.0;
+      }
+      part += dpp<DPP_ROW_HALF_MIRROR>(part);
+      part += dpp<DPP_QUAD_3210>(part);
+      part += dpp<DPP_QUAD_1032>(part);
+      if (i < j && e == (i & 7)) xr[i >> 3] = -tauv[i] * part;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int k = e + 8 * q;
+      Ts[k * TP + j] = k <= j ? xr[q] : 0.0;
     }
   }
   __syncthreads();
-  const int t = threadIdx.x;
-  for (int c = 0; c < IB; ++c) {
-    if (t < c) {
-      double acc = 0.0;
-      for (int s = t; s < c; ++s) acc += Ts[t * TP + s] * Gs[s * TP + c];
-      Ts[t * TP + c] = -tauv[c] * acc;
-    } else if (t < IB) {
-      Ts[t * TP + c] = t == c ? tauv[c] : 0.0;
-    }
-    __syncthreads();
-  }
 }
 
 }  // namespace tqr
