@@ -58,6 +58,10 @@ __device__ unsigned long long g_pstamps[8];
 #define STAMP(i) do {} while (0)
 #endif
 
+}  // namespace tqr
+#include "flow.hpp"
+namespace tqr {
+
 template <int B>
 __device__ __forceinline__ double* tw_ptr(const Args& a, int i, int k, int g) {
   using G = Geo<B>;
@@ -291,6 +295,172 @@ static void get_kernels(kfn* p, kfn* u, kfn* t) {
   *u = k_update<B, S>;
   *t = k_build_t<B, S>;
 }
+typedef void (*ffn)(FlowArgs);
+template <int B, typename S>
+static ffn get_flow() { return k_flow<B, S>; }
+static size_t lds_flow(int b) {
+  int d = 0;
+  switch (b) {
+    case 16: d = flow_lds_doubles<16>(); break;
+    case 32: d = flow_lds_doubles<32>(); break;
+    case 64: d = flow_lds_doubles<64>(); break;
+    case 128: d = flow_lds_doubles<128>(); break;
+    case 256: d = flow_lds_doubles<256>(); break;
+  }
+  return (size_t)d * sizeof(double) + 16;
+}
+static ffn resolve_flow(int b, int dtype) {
+  ffn f = nullptr;
+#define TQR_F(BB) \
+  case BB: f = dtype == TQR_F64 ? get_flow<BB, double>() : get_flow<BB, float>(); break;
+  switch (b) { TQR_F(16) TQR_F(32) TQR_F(64) TQR_F(128) TQR_F(256) }
+#undef TQR_F
+  if (f && hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_flow(b)) != hipSuccess)
+    return nullptr;
+  return f;
+}
+
+// ---------------------------------------------------------------------------------------
+// Flow task list: panel tasks P(i,k) (i == k: GEQRT) and chain segments C(k,j,s,e), ordered
+// by an as-soon-as-possible start-time estimate of the pipelined DAG (unit = one chain
+// element), then checked to be topological (else the always-valid step-major order is used).
+// ---------------------------------------------------------------------------------------
+struct FlowPlan {
+  std::vector<Item> items;
+  bool est_order = false;
+};
+
+static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
+  const int kmax = std::min(p, q), ns = (b + 63) / 64, ng = b / (b < 32 ? b : 32);
+  const double Tg = 0.7, Te = 1.0;
+  // fin_elem[k][i][j] (strips move together in the estimate): finish of chain element (i,j,k)
+  auto id3 = [&](int k, int i, int j) { return ((size_t)k * p + i) * q + j; };
+  std::vector<double> fin((size_t)kmax * p * q, 0.0), pstart((size_t)kmax * p, 0.0);
+  auto fin_prev = [&](int k, int i, int j) { return k > 0 ? fin[id3(k - 1, i, j)] : 0.0; };
+  struct T { double est; int ord; Item it; };
+  std::vector<T> tl;
+  for (int k = 0; k < kmax; ++k) {
+    // panel
+    double ps = fin_prev(k, k, k);
+    pstart[(size_t)k * p + k] = ps;
+    tl.push_back({ps, 0, Item{QRS, k, k, k}});
+    for (int i = k + 1; i < p; ++i) {
+      double st = std::max(fin_prev(k, i, k), pstart[(size_t)k * p + i - 1] + Tg);
+      pstart[(size_t)k * p + i] = st;
+      tl.push_back({st, 0, Item{QRD, i, k, k}});
+    }
+    // chains
+    for (int j = k + 1; j < q; ++j) {
+      double t0 = std::max(fin_prev(k, k, j), pstart[(size_t)k * p + k] + Tg);
+      double prev = t0 + 0.5 * Te;  // UNMQR
+      fin[id3(k, k, j)] = prev;
+      std::vector<double> seg_start;
+      seg_start.push_back(t0);
+      for (int i = k + 1; i < p; ++i) {
+        double st = std::max({prev, fin_prev(k, i, j), pstart[(size_t)k * p + i] + Tg});
+        if ((i - k - 1) % seglen == 0 && i > k + 1) seg_start.push_back(st);
+        double f = std::max(st + Te, pstart[(size_t)k * p + i] + ng * Tg + Te / ng);
+        fin[id3(k, i, j)] = f;
+        prev = f;
+      }
+      int nseg = p - k - 1 > 0 ? (p - k - 1 + seglen - 1) / seglen : 1;
+      for (int e = 0; e < nseg; ++e) {
+        int i0 = k + 1 + e * seglen, i1 = std::min(p, i0 + seglen);
+        if (p - k - 1 == 0) { i0 = p; i1 = p; }
+        for (int s = 0; s < ns; ++s)
+          tl.push_back({seg_start[std::min<size_t>(e, seg_start.size() - 1)], 1,
+                        Item{T_CHAIN | (s << 8), i0 | (i1 << 16), j, k | (e << 16)}});
+      }
+    }
+  }
+  auto valid = [&](const std::vector<Item>& L) {
+    // position of every task; check deps precede
+    std::map<std::tuple<int, int, int, int, int>, int> pos;  // (type, a, b, c, d)
+    for (int x = 0; x < (int)L.size(); ++x) {
+      const Item& it = L[x];
+      int ty = it.ts & 0xff;
+      if (ty == T_CHAIN) pos[std::make_tuple(T_CHAIN, it.k & 0xffff, it.m, (it.ts >> 8) & 0xff, it.k >> 16)] = x;
+      else pos[std::make_tuple(0, it.l, it.k, 0, 0)] = x;
+    }
+    auto seg_of = [&](int k, int i) { return (i - k - 1) / seglen; };
+    for (int x = 0; x < (int)L.size(); ++x) {
+      const Item& it = L[x];
+      int ty = it.ts & 0xff;
+      std::vector<int> deps;
+      if (ty == T_CHAIN) {
+        int s = (it.ts >> 8) & 0xff, k = it.k & 0xffff, e = it.k >> 16, j = it.m, i0 = it.l & 0xffff, i1 = it.l >> 16;
+        if (e > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k, j, s, e - 1)]);
+        else deps.push_back(pos[std::make_tuple(0, k, k, 0, 0)]);
+        if (e == 0 && k > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, k))]);
+        for (int i = i0; i < i1; ++i) {
+          deps.push_back(pos[std::make_tuple(0, i, k, 0, 0)]);
+          if (k > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, i))]);
+        }
+      } else {
+        int i = it.l, k = it.k;
+        if (i > k) deps.push_back(pos[std::make_tuple(0, i - 1, k, 0, 0)]);
+        if (k > 0)
+          for (int s = 0; s < ns; ++s) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, k, s, seg_of(k - 1, i))]);
+      }
+      for (int d : deps)
+        if (d >= x) {
+          if (getenv("TQR_DEBUG_PLAN")) {
+            const Item& dd = L[d];
+            fprintf(stderr, "flow plan: task %d (ts=%x l=%x m=%d k=%x) depends on later task %d (ts=%x l=%x m=%d k=%x)\n",
+                    x, it.ts, it.l, it.m, it.k, d, dd.ts, dd.l, dd.m, dd.k);
+          }
+          return false;
+        }
+    }
+    return true;
+  };
+  // bump every task's key past its dependencies' keys (tl is topological, step-major), so the
+  // estimated-time order is topological by construction
+  {
+    std::map<std::tuple<int, int, int, int, int>, int> idx;
+    for (int x = 0; x < (int)tl.size(); ++x) {
+      const Item& it = tl[x].it;
+      int ty = it.ts & 0xff;
+      if (ty == T_CHAIN) idx[std::make_tuple(T_CHAIN, it.k & 0xffff, it.m, (it.ts >> 8) & 0xff, it.k >> 16)] = x;
+      else idx[std::make_tuple(0, it.l, it.k, 0, 0)] = x;
+    }
+    auto seg_of = [&](int k, int i) { return (i - k - 1) / seglen; };
+    for (int x = 0; x < (int)tl.size(); ++x) {
+      const Item& it = tl[x].it;
+      int ty = it.ts & 0xff;
+      double key = tl[x].est;
+      auto bump = [&](int d) { key = std::max(key, tl[d].est + 1e-6); };
+      if (ty == T_CHAIN) {
+        int s = (it.ts >> 8) & 0xff, k = it.k & 0xffff, e = it.k >> 16, j = it.m, i0 = it.l & 0xffff, i1 = it.l >> 16;
+        if (e > 0) bump(idx[std::make_tuple(T_CHAIN, k, j, s, e - 1)]);
+        else bump(idx[std::make_tuple(0, k, k, 0, 0)]);
+        if (e == 0 && k > 0) bump(idx[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, k))]);
+        for (int i = i0; i < i1; ++i) {
+          bump(idx[std::make_tuple(0, i, k, 0, 0)]);
+          if (k > 0) bump(idx[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, i))]);
+        }
+      } else {
+        int i = it.l, k = it.k;
+        if (i > k) bump(idx[std::make_tuple(0, i - 1, k, 0, 0)]);
+        if (k > 0)
+          for (int s = 0; s < ns; ++s) bump(idx[std::make_tuple(T_CHAIN, k - 1, k, s, seg_of(k - 1, i))]);
+      }
+      tl[x].est = key;
+    }
+  }
+  std::vector<T> sorted = tl;
+  std::stable_sort(sorted.begin(), sorted.end(), [](const T& x, const T& y) {
+    if (x.est != y.est) return x.est < y.est;
+    return x.ord < y.ord;
+  });
+  fp.items.clear();
+  for (auto& t : sorted) fp.items.push_back(t.it);
+  fp.est_order = valid(fp.items);
+  if (!fp.est_order) {  // step-major: always topological
+    fp.items.clear();
+    for (auto& t : tl) fp.items.push_back(t.it);
+  }
+}
 static size_t lds_build_t(int b) {
   int ib = b < 32 ? b : 32;
   return ((size_t)b * (ib + 2) + 6 * (size_t)ib * (ib + 1) + ib + 2) * sizeof(double);
@@ -329,6 +499,16 @@ struct tqr_plan {
   kfn kp = nullptr, ku = nullptr;
   size_t ldsP = 0, ldsU = 0;
   int profile = 0;
+  // flow engine
+  int engine = 1;          // 1 = persistent dataflow (default), 0 = wave-batched launches
+  Item* d_flow = nullptr;
+  int nflow = 0;
+  int* d_sync = nullptr;   // next, err, Rc, Tc, Ac
+  size_t sync_ints = 0;
+  int ns = 1, ng = 1, grid = 256, est_order = 0;
+  ffn kflow = nullptr;
+  size_t ldsF = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> prof_ev;  // pairs per launch when profiling
   std::vector<int> prof_kind;
   int nl_u = 0, nl_p = 0;
@@ -387,6 +567,10 @@ void tqr_plan_destroy(tqr_plan* pl) {
   if (pl->evP) (void)hipEventDestroy(pl->evP);
   if (pl->evU) (void)hipEventDestroy(pl->evU);
   if (pl->evStart) (void)hipEventDestroy(pl->evStart);
+  if (pl->d_flow) (void)hipFree(pl->d_flow);
+  if (pl->d_sync) (void)hipFree(pl->d_sync);
+  if (pl->ev0) (void)hipEventDestroy(pl->ev0);
+  if (pl->ev1) (void)hipEventDestroy(pl->ev1);
   for (auto e : pl->prof_ev) (void)hipEventDestroy(e);
   delete pl;
 }
@@ -457,6 +641,37 @@ kfn kt;
   return TQR_OK;
 }
 
+int tqr_plan_status(tqr_plan* pl, void* stream) {
+  if (!pl) return TQR_EINVAL;
+  if (pl->engine != 1) return TQR_OK;
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  int err = 0;
+  HIPCHK(hipMemcpy(&err, pl->d_sync + 1, sizeof(int), hipMemcpyDeviceToHost));
+  if (err) {
+    fprintf(stderr, "tqr: dataflow engine aborted (error word %d: a dependency wait timed out)\n", err);
+    return TQR_EHIP;
+  }
+  return TQR_OK;
+}
+
+int tqr_flow_plan_check(int M, int N, int b, int seglen, int* ntasks, int* est_order) {
+  if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1) return TQR_EINVAL;
+  FlowPlan fp;
+  build_flow_plan(M, N, b, seglen, fp);
+  if (ntasks) *ntasks = (int)fp.items.size();
+  if (est_order) *est_order = fp.est_order;
+  return TQR_OK;
+}
+
+int tqr_plan_info(const tqr_plan* pl, int* engine, int* ntasks, int* est_order, int* grid) {
+  if (!pl) return TQR_EINVAL;
+  if (engine) *engine = pl->engine;
+  if (ntasks) *ntasks = pl->engine == 1 ? pl->nflow : (int)pl->off_u.back();
+  if (est_order) *est_order = pl->est_order;
+  if (grid) *grid = pl->grid;
+  return TQR_OK;
+}
+
 int tqr_plan_set_profile(tqr_plan* pl, int on) {
   if (!pl) return TQR_EINVAL;
   pl->profile = on;
@@ -475,6 +690,26 @@ int tqr_plan_stats(const tqr_plan* pl, int* nu, double* msu, int* np, double* ms
 int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream) {
   if (!pl || !dA || !dtau || ldda < pl->m) return TQR_EINVAL;
   hipStream_t cs = (hipStream_t)stream;
+  if (pl->engine == 1) {
+    FlowArgs f;
+    f.A = dA; f.tau = dtau; f.Tw = pl->d_T; f.tasks = pl->d_flow; f.ntasks = pl->nflow; f.ldm = ldda;
+    f.m = pl->m; f.p = pl->p; f.q = pl->q; f.kmax = pl->kmax; f.ns = pl->ns;
+    f.next = pl->d_sync; f.err = pl->d_sync + 1; f.Rc = pl->d_sync + 2;
+    f.Tc = f.Rc + (size_t)pl->kmax * pl->ng;
+    f.Ac = f.Tc + (size_t)pl->p * pl->q * pl->ns;
+    HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
+    if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
+    hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(FLOW_NT), pl->ldsF, cs, f);
+    HIPCHK(hipGetLastError());
+    if (pl->profile) {
+      HIPCHK(hipEventRecord(pl->ev1, cs));
+      HIPCHK(hipEventSynchronize(pl->ev1));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, pl->ev0, pl->ev1));
+      pl->nl_u = 1; pl->ms_u = ms; pl->nl_p = 0; pl->ms_p = 0;
+    }
+    return TQR_OK;
+  }
   Args a;
   a.A = dA; a.tau = dtau; a.Tw = pl->d_T; a.ldm = ldda; a.m = pl->m; a.p = pl->p; a.kmax = pl->kmax;
   // both work streams start after everything already queued on the caller's stream
@@ -576,6 +811,7 @@ static int geqrt_host(void* A, void* tau, int m, int n, int ldm, int b, int dtyp
       hipMemset(dT, 0, es * (size_t)m * kmax) != hipSuccess) st = TQR_EHIP;
   if (!st) st = tqr_plan_execute(pl, dA, m, dT, nullptr);
   if (!st && hipDeviceSynchronize() != hipSuccess) st = TQR_EHIP;
+  if (!st) st = tqr_plan_status(pl, nullptr);
   if (!st && hipMemcpy2D(A, es * ldm, dA, es * m, es * m, n, hipMemcpyDeviceToHost) != hipSuccess) st = TQR_EHIP;
   if (!st && tau) {
     // column k of the compact array -> column k*b of the reference tau matrix, rows k*b..m-1

@@ -66,8 +66,13 @@ struct Geo {
 
 template <typename S>
 __device__ __forceinline__ double ld(const S* p) { return (double)*p; }
+// Global stores are write-through (sc1): results are handed to workgroups on other XCDs, and a
+// release fence then has no dirty L2 lines of ours to write back (MI355X_MICROARCH.md,
+// "publish-large").
 template <typename S>
-__device__ __forceinline__ void st(S* p, double v) { *p = (S)v; }
+__device__ __forceinline__ void st(S* p, double v) {
+  __hip_atomic_store(p, (S)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -103,6 +108,8 @@ __device__ __forceinline__ void apply_group(const double* __restrict__ Vs, const
   // Z += V^T X   (A operand: V[4ks+x][4ri+y])
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
+    // bound the scheduler's hoisting of V-image reads (else it lifts ~500 LDS loads and spills)
+    if ((ks & 3) == 0) asm volatile("" ::: "memory");
     if (!HEAD && ks < ks0) continue;
     const double2* vr = reinterpret_cast<const double2*>(Vs + (4 * ks + x) * VP + y * NRI);
     double a[NRI];
@@ -131,6 +138,7 @@ __device__ __forceinline__ void apply_group(const double* __restrict__ Vs, const
   // X -= V W   (A operand: V[4ks+y][4wi+x]); 4 row blocks interleaved to hide MFMA latency.
 #pragma unroll
   for (int kb = 0; kb < NKS; kb += 4) {
+    asm volatile("" ::: "memory");
     if (!HEAD && kb + 3 < ks0) continue;
     double a[4][NRI];
 #pragma unroll

@@ -50,6 +50,18 @@ void tqr_plan_destroy(tqr_plan* plan);
  * Stream-ordered: returns once all work is enqueued. */
 int tqr_plan_execute(tqr_plan* plan, void* dA, int ldda, void* dtau_compact, void* stream);
 
+/* Synchronise `stream` and report whether the last execute completed (the persistent engine
+ * bounds every dependency wait and reports a timeout here instead of hanging). */
+int tqr_plan_status(tqr_plan* plan, void* stream);
+/* engine: 1 = persistent dataflow (default; TQR_ENGINE=waves selects 0 = wave-batched
+ * launches), ntasks: task-list length, est_order: 1 if the start-time-estimate order was
+ * used (else step-major), grid: workgroups of the persistent launch. */
+int tqr_plan_info(const tqr_plan* plan, int* engine, int* ntasks, int* est_order, int* grid);
+
+/* Host-only check of the persistent engine's task list for an M x N tile grid (no GPU):
+ * number of tasks and whether the estimated-start-time order is topological. */
+int tqr_flow_plan_check(int M, int N, int b, int seglen, int* ntasks, int* est_order);
+
 /* Per-launch statistics of the last execute (filled when the plan was created with
  * tqr_plan_set_profile(plan, 1)): number of kernel launches and the summed device time of
  * the trailing-update (TSMQR/UNMQR) and panel (GEQRT/TSQRT) kernels in ms. */

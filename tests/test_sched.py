@@ -72,3 +72,19 @@ def test_total_tasks(tqr):
     assert tqr.lib().tqr_sched_total_tasks(3, 6) == 32  # the reference's calcTotalTasks says 28
     assert tqr.lib().tqr_total_tasks(16384, 16384, 256) == 89440
     assert tqr.lib().tqr_total_tasks(100, 64, 32) == -1
+
+
+@pytest.mark.parametrize("M,N,b,seg", [(64, 64, 256, 8), (32, 32, 128, 8), (8, 8, 64, 8), (256, 64, 256, 8),
+                                       (3, 6, 32, 2), (6, 3, 32, 2), (1, 1, 32, 8), (5, 7, 16, 1), (1, 5, 32, 4)])
+def test_flow_plan_topological(tqr, M, N, b, seg):
+    """The persistent engine's task list (panel tasks + chain segments) is in an order where
+    every task waits only on earlier tasks — the engine's deadlock-freedom condition."""
+    import ctypes
+    n, o = ctypes.c_int(), ctypes.c_int()
+    assert tqr.lib().tqr_flow_plan_check(M, N, b, seg, ctypes.byref(n), ctypes.byref(o)) == 0
+    kmax = min(M, N)
+    ns = (b + 63) // 64
+    panels = sum(M - k for k in range(kmax))
+    chains = sum((N - k - 1) * ns * max(1, -(-(M - k - 1) // seg)) for k in range(kmax))
+    assert n.value == panels + chains
+    assert o.value == 1
