@@ -633,10 +633,43 @@ int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) {
       hipEventCreateWithFlags(&pl->evStart, hipEventDisableTiming) != hipSuccess) {
     tqr_plan_destroy(pl); return TQR_EHIP;
   }
-kfn kt;
+  kfn kt;
   if (resolve(b, dtype, &pl->kp, &pl->ku, &kt) != TQR_OK) { tqr_plan_destroy(pl); return TQR_EHIP; }
   pl->ldsP = lds_panel(b);
   pl->ldsU = lds_update(b);
+  // persistent dataflow engine: task list, progress counters, kernel
+  const char* eng = getenv("TQR_ENGINE");
+  pl->engine = (eng && strcmp(eng, "waves") == 0) ? 0 : 1;
+  pl->ns = (b + 63) / 64;
+  pl->ng = b / ib;
+  {
+    FlowPlan fp;
+    const char* sl = getenv("TQR_SEGLEN");
+    build_flow_plan(pl->p, pl->q, b, sl ? std::max(1, atoi(sl)) : 8, fp);
+    pl->nflow = (int)fp.items.size();
+    pl->est_order = fp.est_order;
+    pl->sync_ints = 2 + (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns + (size_t)pl->kmax * pl->q * pl->ns;
+    if (pl->nflow <= 0 || hipMalloc(&pl->d_flow, sizeof(Item) * pl->nflow) != hipSuccess ||
+        hipMalloc(&pl->d_sync, sizeof(int) * pl->sync_ints) != hipSuccess) {
+      tqr_plan_destroy(pl); return TQR_ENOMEM;
+    }
+    if (hipMemcpy(pl->d_flow, fp.items.data(), sizeof(Item) * pl->nflow, hipMemcpyHostToDevice) != hipSuccess) {
+      tqr_plan_destroy(pl); return TQR_EHIP;
+    }
+    pl->kflow = resolve_flow(b, dtype);
+    pl->ldsF = lds_flow(b);
+    int dev = 0;
+    hipDeviceProp_t pr;
+    if (!pl->kflow || hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&pr, dev) != hipSuccess) {
+      tqr_plan_destroy(pl); return TQR_EHIP;
+    }
+    pl->grid = pr.multiProcessorCount;
+    const char* gs = getenv("TQR_FLOW_GRID");
+    if (gs) pl->grid = std::max(1, atoi(gs));
+    if (hipEventCreate(&pl->ev0) != hipSuccess || hipEventCreate(&pl->ev1) != hipSuccess) {
+      tqr_plan_destroy(pl); return TQR_EHIP;
+    }
+  }
   *out = pl;
   return TQR_OK;
 }
@@ -691,6 +724,7 @@ int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream)
   if (!pl || !dA || !dtau || ldda < pl->m) return TQR_EINVAL;
   hipStream_t cs = (hipStream_t)stream;
   if (pl->engine == 1) {
+    if (!pl->kflow || !pl->d_flow || !pl->d_sync) return TQR_EINVAL;
     FlowArgs f;
     f.A = dA; f.tau = dtau; f.Tw = pl->d_T; f.tasks = pl->d_flow; f.ntasks = pl->nflow; f.ldm = ldda;
     f.m = pl->m; f.p = pl->p; f.q = pl->q; f.kmax = pl->kmax; f.ns = pl->ns;
