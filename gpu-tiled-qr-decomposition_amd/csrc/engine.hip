@@ -58,6 +58,9 @@ __device__ unsigned long long g_pstamps[8];
 #define STAMP(i) do {} while (0)
 #endif
 
+#ifdef TQR_FLOW_STAMPS
+__device__ unsigned long long g_fst[4096 * 8];
+#endif
 }  // namespace tqr
 #include "flow.hpp"
 namespace tqr {
@@ -65,7 +68,7 @@ namespace tqr {
 template <int B>
 __device__ __forceinline__ double* tw_ptr(const Args& a, int i, int k, int g) {
   using G = Geo<B>;
-  return a.Tw + (((size_t)k * a.p + i) * G::NG + g) * (G::IB * G::IB);
+  return a.Tw + (((size_t)k * a.p + i) * G::NG + g) * G::TIMG;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -119,7 +122,7 @@ __global__ __launch_bounds__(NT, 1) void k_panel(Args a) {
       __syncthreads();
       build_t<B>(Vs, tauv, Gs, Ts, Gp, ks0);
       double* tg = tw_ptr<B>(a, k, k, g);
-      for (int idx = t; idx < IB * IB; idx += NT) tg[idx] = Ts[(idx / IB) * TP + idx % IB];
+      for (int idx = t; idx < G::TSZ; idx += NT) tg[idx] = Ts[idx];
       // trailing columns of the tile
       const int nstr = (B - c0 - IB) / 16;
       for (int s = w; s < nstr; s += NT / 64) {
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(NT, 1) void k_panel(Args a) {
       build_t<B>(Vs, tauv, Gs, Ts, Gp, 0);
       STAMP(3);
       double* tg = tw_ptr<B>(a, l, k, g);
-      for (int idx = t; idx < IB * IB; idx += NT) tg[idx] = Ts[(idx / IB) * TP + idx % IB];
+      for (int idx = t; idx < G::TSZ; idx += NT) tg[idx] = Ts[idx];
       const int nstr = (B - c0 - IB) / 16;
       for (int s = w; s < nstr; s += NT / 64) {
         asm volatile("" ::: "memory");  // keep the V-image reads inside the loop (no LICM of ~1k LDS loads)
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(NT, 2) void k_update(Args a) {
 template <int B, typename S>
 __global__ __launch_bounds__(NT, 1) void k_build_t(Args a) {
   using G = Geo<B>;
-  constexpr int IB = G::IB, NG = G::NG, TP = G::TP;
+  constexpr int IB = G::IB, NG = G::NG;
   extern __shared__ __align__(16) double lds[];
   double* Vs = lds;
   double* Ts = Vs + G::VSZ;
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(NT, 1) void k_build_t(Args a) {
   __syncthreads();
   build_t<B>(Vs, tauv, Gs, Ts, Gp, type == QRS ? c0 / 4 : 0);
   double* tg = tw_ptr<B>(a, type == QRS ? k : l, k, g);
-  for (int idx = threadIdx.x; idx < IB * IB; idx += NT) tg[idx] = Ts[(idx / IB) * TP + idx % IB];
+  for (int idx = threadIdx.x; idx < G::TSZ; idx += NT) tg[idx] = Ts[idx];
 }
 
 // RANDZO-distributed synthetic input: ((h mod 201) - 100) / 100 from a splitmix64 hash.
@@ -307,7 +310,7 @@ static size_t lds_flow(int b) {
     case 128: d = flow_lds_doubles<128>(); break;
     case 256: d = flow_lds_doubles<256>(); break;
   }
-  return (size_t)d * sizeof(double) + 16;
+  return (size_t)d * sizeof(double) + 256;  // + task index, FST sums, sync-point verdicts, Rc view
 }
 static ffn resolve_flow(int b, int dtype) {
   ffn f = nullptr;
@@ -332,7 +335,9 @@ struct FlowPlan {
 
 static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
   const int kmax = std::min(p, q), ns = (b + 63) / 64, ng = b / (b < 32 ? b : 32);
-  const double Tg = 0.7, Te = 1.0;
+  // cost model (unit: one chain element): Tg = one panel group-step; tunable for experiments
+  const char* eg = getenv("TQR_TG");
+  const double Tg = eg ? atof(eg) : 1.4, Te = 1.0;
   // fin_elem[k][i][j] (strips move together in the estimate): finish of chain element (i,j,k)
   auto id3 = [&](int k, int i, int j) { return ((size_t)k * p + i) * q + j; };
   std::vector<double> fin((size_t)kmax * p * q, 0.0), pstart((size_t)kmax * p, 0.0);
@@ -482,6 +487,15 @@ static int resolve(int b, int dtype, kfn* kp, kfn* ku, kfn* kt) {
 }
 
 static bool valid_b(int b) { return b == 16 || b == 32 || b == 64 || b == 128 || b == 256; }
+// workspace slot sizes (doubles) of Geo<b>::TIMG / VIMG
+static size_t timg_doubles(int b) {
+  const size_t ib = b < 32 ? b : 32;
+  return (ib * (ib + 1) + 127) / 128 * 128;
+}
+static size_t vimg_doubles(int b) {
+  const size_t ib = b < 32 ? b : 32;
+  return ((size_t)b * (ib + 2) + 127) / 128 * 128;
+}
 
 }  // namespace tqr
 
@@ -494,6 +508,7 @@ struct tqr_plan {
   Item* d_items_p = nullptr;
   Item* d_items_u = nullptr;
   double* d_T = nullptr;
+  double* d_V = nullptr;   // V images (flow engine)
   hipStream_t sP = nullptr, sU = nullptr;
   hipEvent_t evP = nullptr, evU = nullptr, evStart = nullptr;
   kfn kp = nullptr, ku = nullptr;
@@ -562,6 +577,7 @@ void tqr_plan_destroy(tqr_plan* pl) {
   if (pl->d_items_p) (void)hipFree(pl->d_items_p);
   if (pl->d_items_u) (void)hipFree(pl->d_items_u);
   if (pl->d_T) (void)hipFree(pl->d_T);
+  if (pl->d_V) (void)hipFree(pl->d_V);
   if (pl->sP) (void)hipStreamDestroy(pl->sP);
   if (pl->sU) (void)hipStreamDestroy(pl->sU);
   if (pl->evP) (void)hipEventDestroy(pl->evP);
@@ -613,7 +629,7 @@ int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) {
   tqr_sched_plan_free(&sp);
 
   int ib = b < 32 ? b : 32;
-  size_t tw = (size_t)pl->p * pl->kmax * (b / ib) * ib * ib * sizeof(double);
+  size_t tw = (size_t)pl->p * pl->kmax * (b / ib) * timg_doubles(b) * sizeof(double);
   if (hipMalloc(&pl->d_items_p, std::max<size_t>(1, ip.size()) * sizeof(Item)) != hipSuccess ||
       hipMalloc(&pl->d_items_u, std::max<size_t>(1, iu.size()) * sizeof(Item)) != hipSuccess ||
       hipMalloc(&pl->d_T, tw) != hipSuccess) {
@@ -649,7 +665,9 @@ int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) {
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
     pl->sync_ints = 2 + (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns + (size_t)pl->kmax * pl->q * pl->ns;
+    const size_t vw = (size_t)pl->p * pl->kmax * pl->ng * vimg_doubles(b) * sizeof(double);
     if (pl->nflow <= 0 || hipMalloc(&pl->d_flow, sizeof(Item) * pl->nflow) != hipSuccess ||
+        hipMalloc(&pl->d_V, vw) != hipSuccess ||
         hipMalloc(&pl->d_sync, sizeof(int) * pl->sync_ints) != hipSuccess) {
       tqr_plan_destroy(pl); return TQR_ENOMEM;
     }
@@ -726,7 +744,7 @@ int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream)
   if (pl->engine == 1) {
     if (!pl->kflow || !pl->d_flow || !pl->d_sync) return TQR_EINVAL;
     FlowArgs f;
-    f.A = dA; f.tau = dtau; f.Tw = pl->d_T; f.tasks = pl->d_flow; f.ntasks = pl->nflow; f.ldm = ldda;
+    f.A = dA; f.tau = dtau; f.Tw = pl->d_T; f.Vw = pl->d_V; f.tasks = pl->d_flow; f.ntasks = pl->nflow; f.ldm = ldda;
     f.m = pl->m; f.p = pl->p; f.q = pl->q; f.kmax = pl->kmax; f.ns = pl->ns;
     f.next = pl->d_sync; f.err = pl->d_sync + 1; f.Rc = pl->d_sync + 2;
     f.Tc = f.Rc + (size_t)pl->kmax * pl->ng;
@@ -897,7 +915,7 @@ struct TileRun {
     if ((st = resolve(b, dtype, &kp, &ku, &kt))) return st;
     int ib = b < 32 ? b : 32;
     if (hipMalloc(&dA, es * mr * nc) != hipSuccess || hipMalloc(&dtau, es * mr) != hipSuccess ||
-        hipMalloc(&dT, sizeof(double) * (size_t)p * b * ib) != hipSuccess || hipMalloc(&dit, sizeof(Item) * 4) != hipSuccess)
+        hipMalloc(&dT, sizeof(double) * (size_t)p * (b / ib) * timg_doubles(b)) != hipSuccess || hipMalloc(&dit, sizeof(Item) * 4) != hipSuccess)
       return TQR_ENOMEM;
     if (hipMemset(dA, 0, es * mr * nc) != hipSuccess || hipMemset(dtau, 0, es * mr) != hipSuccess) return TQR_EHIP;
     return TQR_OK;
@@ -1009,6 +1027,15 @@ extern "C" int tqr_debug_stamps(unsigned long long* out, int reset) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) != hipSuccess) return TQR_EHIP;
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_pstamps), z, sizeof z) != hipSuccess) return TQR_EHIP;
   }
+  return TQR_OK;
+}
+#endif
+
+#ifdef TQR_FLOW_STAMPS
+// per-workgroup activity sums of the last k_flow launch (8 categories, flow.hpp FST)
+extern "C" int tqr_debug_flow_stamps(unsigned long long* out, int nblocks) {
+  if (nblocks > 4096) return TQR_EINVAL;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fst), sizeof(unsigned long long) * 8 * nblocks) != hipSuccess) return TQR_EHIP;
   return TQR_OK;
 }
 #endif

@@ -24,13 +24,34 @@
 namespace tqr {
 
 constexpr int T_CHAIN = 4;
+
+// Diagnostic build only (make flowstamps): per-workgroup s_memrealtime sums by activity.
+// Every FST(c) charges the time since the previous stamp to category c (LDS-resident sums,
+// thread 0 only, written to g_fst[blockIdx.x][*] at exit). Categories: 0 chain waits,
+// 1 panel waits, 2 chain head-row I/O, 3 chain apply (with the LDS-DMA issue), 4 chain strip
+// I/O + publish, 5 panel compute, 6 dequeue/dispatch + kernel exit, 7 chain drain + barrier.
+#ifdef TQR_FLOW_STAMPS
+extern __device__ unsigned long long g_fst[];
+#define FST(c)                                                                            \
+  do {                                                                                    \
+    if (threadIdx.x == 0) {                                                               \
+      unsigned long long* l_ = reinterpret_cast<unsigned long long*>(sflag + 1);          \
+      const unsigned long long n_ = __builtin_amdgcn_s_memrealtime();                     \
+      l_[1 + (c)] += n_ - l_[0];                                                          \
+      l_[0] = n_;                                                                         \
+    }                                                                                     \
+  } while (0)
+#else
+#define FST(c) do {} while (0)
+#endif
 constexpr int FLOW_NT = 256;
 constexpr unsigned long long FLOW_TIMEOUT = 500000000ull;  // 5 s of s_memrealtime (100 MHz)
 
 struct FlowArgs {
   void* A;
   void* tau;
-  double* Tw;
+  double* Tw;      // T images, one Geo<B>::TIMG slot per (tile, group)
+  double* Vw;      // V images (the chain's LDS image of each group), one Geo<B>::VIMG slot
   const Item* tasks;
   int ntasks;
   long ldm;
@@ -60,87 +81,128 @@ __device__ __noinline__ bool spin_ge(int* p, int target, int* err) {
   return true;
 }
 
-// all threads: thread 0's verdict, made visible after an agent-scope acquire
-__device__ __forceinline__ bool wg_acquire(bool ok0, int* sflag) {
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    *sflag = ok0 ? 1 : 0;
-  }
+// Hand-off protocol inside the launch (MI355X_MICROARCH.md, visibility "Valid forms", first
+// table row): every handed-off byte is stored sc1 (write-through) and each storing wave drains
+// (vmcnt(0)) before a workgroup barrier, after which ONE lane bumps the counter (agent atomic);
+// a consumer's thread 0 polls the counter relaxed, a barrier follows, and the other waves read the
+// bytes with sc1 loads — no release / acquire fences (each ~1.7 us at one workgroup per CU).
+// The one exception is the chain's LDS-DMA of V/T images (not a register load): those are read
+// behind an agent-scope acquire, taken once per new observation of the panel counters.
+
+// all threads: thread 0's verdict (after its polls)
+__device__ __forceinline__ bool wg_verdict(bool ok0, int* sflag) {
+  if (threadIdx.x == 0) *sflag = ok0 ? 1 : 0;
   __syncthreads();
   const bool ok = *sflag != 0;
   __syncthreads();
   return ok;
 }
 
-// all threads: every wave's stores drained, then thread 0 releases and bumps the counter
+// all threads: every wave's (sc1) stores drained, then thread 0 bumps the counter
 __device__ __forceinline__ void wg_publish(int* p, int delta) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(p, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(p, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int B>
 __device__ __forceinline__ double* flow_tw(const FlowArgs& a, int i, int k, int g) {
   using G = Geo<B>;
-  return a.Tw + (((size_t)k * a.p + i) * G::NG + g) * (G::IB * G::IB);
+  return a.Tw + (((size_t)k * a.p + i) * G::NG + g) * G::TIMG;
+}
+template <int B>
+__device__ __forceinline__ double* flow_vw(const FlowArgs& a, int i, int k, int g) {
+  using G = Geo<B>;
+  return a.Vw + (((size_t)k * a.p + i) * G::NG + g) * G::VIMG;
 }
 
-// ---- register-staged prefetch of one reflector group (V block + T) -------------------------
+// ---- LDS-DMA staging of one reflector group ------------------------------------------------
+// The producer (flow_panel) stores every group's V image (row-major, permuted columns, pitch VP,
+// GE part made explicit) and T image into the workspaces; a consumer copies both verbatim with
+// global_load_lds_dwordx4 (1 KiB per wave-instruction, lane-linear), so the staging costs no
+// VGPRs, no ds_write pass and runs under the MFMA phase that follows (CDNA4 LDS-DMA,
+// cdna_hip_programming.md §5).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+// DMA job of one group for apply_zw's hook: step m issues this wave's m-th LDS-DMA instruction
+// (V image instructions first, then T), so the issue cost hides under the MFMA stream.
 template <int B>
-struct GroupRegs {
-  static constexpr int NV = B * Geo<B>::IB / FLOW_NT;  // V values per thread
-  static constexpr int NTT = (Geo<B>::IB * Geo<B>::IB + FLOW_NT - 1) / FLOW_NT;
-  double v[NV > 0 ? NV : 1];
-  double t[NTT];
+struct DmaJob {
+  static constexpr int NIV = Geo<B>::VIMG / 128, NIT = Geo<B>::TIMG / 128;
+  static constexpr int PV = (NIV + 3) / 4, PT = (NIT + 3) / 4;
+  static constexpr int STEPS = PV + PT;
+  double* dst;
+  const double* v;
+  const double* t;
+  bool on;
+  __device__ __forceinline__ void step(int m) const {
+    if (!on) return;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (m < PV) {
+      const int u = w + 4 * m;
+      if (u < NIV)
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(v + u * 128 + 2 * lane), (lds_void_t*)(dst + u * 128), 16, 0, 16);
+    } else if (m < STEPS) {
+      const int u = w + 4 * (m - PV);
+      if (u < NIT)
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(t + u * 128 + 2 * lane),
+                                         (lds_void_t*)(dst + Geo<B>::VIMG + u * 128), 16, 0, 16);
+    }
+  }
 };
 
-// TS-type (V_B dense) or GE-type (explicit unit lower) group g of tile `vt`
-template <int B, bool GE, typename S>
-__device__ __forceinline__ void group_load(GroupRegs<B>& R, const S* __restrict__ vt, size_t ldm, int c0,
-                                           const double* __restrict__ tg) {
-  using G = Geo<B>;
-  // thread t reads rows r = (t + 256u) % B of columns c0 + (t + 256u) / B: a running pointer,
-  // made opaque per step so the compiler does not keep 32 precomputed 64-bit offsets alive
-  constexpr int CPS = FLOW_NT / B > 0 ? FLOW_NT / B : 1;  // columns per step (B <= 256)
-  const int r = threadIdx.x % B;
-  const S* pv = vt + (size_t)(c0 + threadIdx.x / B) * ldm + r;
-#pragma unroll
-  for (int u = 0; u < GroupRegs<B>::NV; ++u) {
-    const int d = c0 + (threadIdx.x + FLOW_NT * u) / B;
-    if (GE) R.v[u] = r <= d ? 0.0 : ld(pv);
-    else R.v[u] = ld(pv);
-    pv += (size_t)CPS * ldm;
-    asm volatile("" : "+v"(pv));
-  }
-#pragma unroll
-  for (int u = 0; u < GroupRegs<B>::NTT; ++u) {
-    const int idx = threadIdx.x + FLOW_NT * u;
-    R.t[u] = idx < G::IB * G::IB ? tg[idx] : 0.0;
-  }
+// All threads: thread 0 has polled its dependencies (verdict ok0, and acquired if it needed
+// to). Optionally drain this wave's vector-memory operations (its LDS-DMA landed, loads and
+// stores complete), one raw barrier (no implicit vmcnt(0)), then every wave reads the verdict
+// from a parity-alternating LDS slot (a slot is rewritten only after the next barrier).
+template <bool DRAIN>
+__device__ __forceinline__ bool sync_point(bool ok0, int* sflag, int& par) {
+  int* slot = sflag + 24 + par;  // LDS tail: [task][flag][FST sums 2..19][..][verdicts 25,26][..][Rc view 33..]
+  par ^= 1;
+  if (threadIdx.x == 0) *slot = ok0 ? 1 : 0;
+  if (DRAIN) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  return *(volatile int*)slot != 0;
 }
-template <int B, bool GE>
-__device__ __forceinline__ void group_commit(const GroupRegs<B>& R, double* Vs, double* Ts, int c0) {
-  using G = Geo<B>;
-#pragma unroll
-  for (int u = 0; u < GroupRegs<B>::NV; ++u) {
-    const int idx = threadIdx.x + FLOW_NT * u, r = idx % B, c = idx / B;
-    Vs[r * G::VP + G::pc(c)] = (GE && r == c0 + c) ? 1.0 : R.v[u];
-  }
-#pragma unroll
-  for (int u = 0; u < GroupRegs<B>::NTT; ++u) {
-    const int idx = threadIdx.x + FLOW_NT * u;
-    if (idx < G::IB * G::IB) Ts[(idx / G::IB) * G::TP + idx % G::IB] = R.t[u];
-  }
+// thread 0, after a draining sync point (every wave's sc1 stores complete): bump a counter
+__device__ __forceinline__ void publish_after_drain(int* p, int delta) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(p, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// Thread 0's view of one panel's group counters Rc[k][0..NG): rv[g] (LDS, thread 0 only) holds
+// an observed value, so the V/T images of any member < rv[g] of group g may be LDS-DMA'd.
+// ensure(g, need) re-reads the row (one round trip) only when rv[g] < need. No acquire fence:
+// the images are write-once inside a launch (one producer, stored sc1 and drained before its
+// counter add), no workgroup reads a slot before observing its counter, and the DMA itself is
+// an sc1 (L1-bypassing) load — so no CU can hold a stale copy of an image line.
+template <int NG>
+struct PanelView {
+  int* rv;
+  __device__ __forceinline__ void init(int* lds_words) {
+    rv = lds_words;
+    if (threadIdx.x == 0)
+      for (int g = 0; g < NG; ++g) rv[g] = 0;
+  }
+  __device__ __forceinline__ bool ensure(int* rc, int g, int need, int* err) {
+    if (rv[g] >= need) return true;
+    int v[NG];
+#pragma unroll
+    for (int x = 0; x < NG; ++x) v[x] = ld_relaxed(rc + x);
+#pragma unroll
+    for (int x = 0; x < NG; ++x) rv[x] = v[x];
+    if (rv[g] < need) {
+      if (!spin_ge(rc + g, need, err)) return false;
+      rv[g] = ld_relaxed(rc + g);
+    }
+    return true;
+  }
+};
 
 // ---- panel tasks ---------------------------------------------------------------------------
 template <int B, typename S>
-__device__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* lds, int* sflag) {
+__device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* lds, int* sflag) {
   using G = Geo<B>;
   constexpr int IB = G::IB, VP = G::VP, TP = G::TP, NG = G::NG;
   double* Vs = lds;
@@ -158,36 +220,40 @@ __device__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* ld
   const bool qrs = type == QRS;
   S* Bt = qrs ? Rt : A + (size_t)k * B * ldm + (size_t)l * B;
   const int pos = qrs ? 0 : l - k;  // position in the panel chain
+  FST(6);
   // the tile(s) must have received step k-1 on every strip
   {
     bool ok = true;
     if (t == 0 && k > 0)
       for (int s = 0; s < a.ns && ok; ++s) ok = spin_ge(&a.Tc[((size_t)(qrs ? k : l) * a.q + k) * a.ns + s], k, a.err);
-    if (!wg_acquire(ok, sflag)) return;
+    if (!wg_verdict(ok, sflag)) return;
   }
+  FST(1);
   double X[G::NKS];
   double H[G::NRI];
   for (int g = 0; g < NG; ++g) {
     const int c0 = g * IB, ks0 = c0 / 4;
     if (!qrs) {  // R_kk rows of group g as left by the previous chain member
+      FST(5);
       const bool ok = t == 0 ? spin_ge(&a.Rc[(size_t)k * NG + g], pos, a.err) : true;
-      if (!wg_acquire(ok, sflag)) return;
+      if (!wg_verdict(ok, sflag)) return;
+      FST(1);
     }
     if (qrs) {
 #pragma unroll 8
       for (int idx = t; idx < B * IB; idx += FLOW_NT) {
         const int r = idx % B, c = idx / B;
-        Vs[r * VP + G::pc(c)] = r >= c0 ? ld(Rt + (size_t)(c0 + c) * ldm + r) : 0.0;
+        Vs[r * VP + G::pc(c)] = r >= c0 ? ldc(Rt + (size_t)(c0 + c) * ldm + r) : 0.0;
       }
     } else {
 #pragma unroll 8
       for (int idx = t; idx < B * IB; idx += FLOW_NT) {
         const int r = idx % B, c = idx / B;
-        Vs[r * VP + G::pc(c)] = ld(Bt + (size_t)(c0 + c) * ldm + r);
+        Vs[r * VP + G::pc(c)] = ldc(Bt + (size_t)(c0 + c) * ldm + r);
       }
       for (int idx = t; idx < IB * IB; idx += FLOW_NT) {
         const int r = idx % IB, c = idx / IB;
-        if (r <= c) Hs[r * TP + c] = ld(Rt + (size_t)(c0 + c) * ldm + c0 + r);
+        if (r <= c) Hs[r * TP + c] = ldc(Rt + (size_t)(c0 + c) * ldm + c0 + r);
       }
     }
     __syncthreads();
@@ -218,19 +284,23 @@ __device__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* ld
       __syncthreads();
     }
     build_t<B>(Vs, tauv, Gs, Ts, Gp, qrs ? ks0 : 0);
-    double* tg = flow_tw<B>(a, qrs ? k : l, k, g);
-    for (int idx = t; idx < IB * IB; idx += FLOW_NT) st(tg + idx, Ts[(idx / IB) * TP + idx % IB]);
+    {  // V image (explicit) and T image of this group for the chains (LDS-DMA sources)
+      double* tg = flow_tw<B>(a, qrs ? k : l, k, g);
+      double* vg = flow_vw<B>(a, qrs ? k : l, k, g);
+      for (int idx = t; idx < G::TSZ; idx += FLOW_NT) st(tg + idx, Ts[idx]);
+      for (int idx = t; idx < G::VSZ; idx += FLOW_NT) st(vg + idx, Vs[vimg_row(idx / VP) * VP + idx % VP]);
+    }
     const int nstr = (B - c0 - IB) / 16;
     for (int s = w; s < nstr; s += FLOW_NT / 64) {
       asm volatile("" ::: "memory");
       const int col = c0 + IB + 16 * s;
       if (qrs) {
-        load_strip<B>(X, Rt, ldm, col, ks0);
+        load_strip<B, S, true>(X, Rt, ldm, col, ks0);
         apply_group<B, false>(Vs, Ts, X, H, ks0);
         store_strip<B>(X, Rt, ldm, col, ks0);
       } else {
-        load_strip<B>(X, Bt, ldm, col, 0);
-        load_head<B>(H, Rt, ldm, c0, col);
+        load_strip<B, S, true>(X, Bt, ldm, col, 0);
+        load_head<B, S, true>(H, Rt, ldm, c0, col);
         apply_group<B, true>(Vs, Ts, X, H, 0);
         store_strip<B>(X, Bt, ldm, col, 0);
         store_head<B>(H, Rt, ldm, c0, col);
@@ -238,88 +308,137 @@ __device__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* ld
     }
     wg_publish(&a.Rc[(size_t)k * NG + g], 1);
   }
+  FST(5);
 }
 
 // ---- chain tasks ---------------------------------------------------------------------------
+// Elements: UNMQR(k,j) (segment 0 only, GE-type, the strip of tile (k,j) is X) and TSMQR(i,j,k)
+// for i in [i0,i1) (TS-type: X = strip of tile (i,j), head rows = strip of tile (k,j), group by
+// group, prefetched one group ahead into registers). Per reflector group g, in every wave:
+//   sync point (drain: DMA(g) landed, loads/stores done; thread 0 made sure the images of the
+//   next DMA are published and covered by an acquire)
+//   phase 1: Z, W, H (apply_zw); store H(g), load H(g+1)
+//   phase 2: X += V W (apply_x), with DMA(g+1) (or group 0 of the next element) issued inside
+//   its MFMA stream into the other LDS buffer.
+// The tile-strip counter Tc of an element is published after the next element's first drain
+// (its stores are complete by then), so no wave waits for its own stores to land.
 template <int B, typename S>
-__device__ void flow_chain(const FlowArgs& a, int s, int i0, int i1, int j, int k, int seg, double* lds,
-                           int* sflag) {
+__device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1, int j, int k, int seg, double* lds,
+                                        int* sflag) {
   using G = Geo<B>;
-  constexpr int IB = G::IB, NG = G::NG;
-  // double-buffered V/T images: buffer b at lds + b * (VSZ + TSZ)
-  auto Vb = [&](int b) { return lds + b * (G::VSZ + G::TSZ); };
-  auto Tb = [&](int b) { return lds + b * (G::VSZ + G::TSZ) + G::VSZ; };
+  constexpr int IB = G::IB, NG = G::NG, BUF = G::VIMG + G::TIMG;
   S* A = (S*)a.A;
   const size_t ldm = a.ldm;
   const int t = threadIdx.x, w = t >> 6;
   const int col = s * 64 + 16 * w;  // this wave's 16 columns inside the tile
   const bool active = col < B;
   S* At = A + (size_t)j * B * ldm + (size_t)k * B;  // tile (k,j): the chain's head rows
-  const S* Vk = A + (size_t)k * B * ldm + (size_t)k * B;
-  double X[G::NKS];
-  double H[G::NRI];
-  GroupRegs<B> R;
-  int* const tc_kj = &a.Tc[((size_t)k * a.q + j) * a.ns + s];
+  int* const rc = &a.Rc[(size_t)k * NG];
   int* const ac = &a.Ac[((size_t)k * a.q + j) * a.ns + s];
-  int buf = 0;
-
-  if (seg == 0) {
-    // UNMQR of tile (k,j) with GEQRT(k): the strip of tile (k,j) is in X
-    bool ok = t == 0 ? (k == 0 || spin_ge(tc_kj, k, a.err)) : true;
-    ok = ok && (t != 0 || spin_ge(&a.Rc[(size_t)k * NG + 0], 1, a.err));
-    if (!wg_acquire(ok, sflag)) return;
-    if (active) load_strip<B>(X, At, ldm, col, 0);
-    group_load<B, true>(R, Vk, ldm, 0, flow_tw<B>(a, k, k, 0));
-    for (int g = 0; g < NG; ++g) {
-      group_commit<B, true>(R, Vb(buf), Tb(buf), g * IB);
-      __syncthreads();
-      if (g + 1 < NG) {
-        const bool okg = t == 0 ? spin_ge(&a.Rc[(size_t)k * NG + g + 1], 1, a.err) : true;
-        if (!wg_acquire(okg, sflag)) return;
-        group_load<B, true>(R, Vk, ldm, (g + 1) * IB, flow_tw<B>(a, k, k, g + 1));
+  auto tc = [&](int i) { return &a.Tc[((size_t)i * a.q + j) * a.ns + s]; };
+  double X[G::NKS];
+  double H[G::NRI], Hn[G::NRI], W[G::NRI];
+  int buf = 0, par = 0;
+  int* pending = nullptr;
+  bool dma_next = false;  // group 0 of the next element already in flight
+  PanelView<NG> pv;
+  pv.init(sflag + 32);
+  FST(6);
+  const int ifirst = seg == 0 ? k : i0;
+  for (int i = ifirst; i < i1 || i == k; i = (i == k ? i0 : i + 1)) {
+    const bool ts = i != k;
+    const int need = i - k + 1;  // members of panel k that must have finished a group
+    {
+      bool ok = true;
+      if (t == 0) {
+        if (i == ifirst && seg > 0) ok = spin_ge(ac, seg, a.err);
+        if (ok && k > 0) ok = spin_ge(tc(i), k, a.err);
+        if (ok && !dma_next) ok = pv.ensure(rc, 0, need, a.err);
       }
-      if (active) apply_group<B, false>(Vb(buf), Tb(buf), X, H, g * IB / 4);
-      buf ^= 1;
+      FST(0);
+      if (!sync_point<false>(ok, sflag, par)) return;
     }
-    if (active) store_strip<B>(X, At, ldm, col, 0);
-    __syncthreads();
-  } else {
-    const bool ok = t == 0 ? spin_ge(ac, seg, a.err) : true;
-    if (!wg_acquire(ok, sflag)) return;
-  }
-  for (int i = i0; i < i1; ++i) {
-    // tile (i,j) strip at step k-1, and TSQRT(i,k) group 0
-    const int need = i - k + 1;
-    int* tc_ij = &a.Tc[((size_t)i * a.q + j) * a.ns + s];
-    bool ok = true;
-    if (t == 0) {
-      if (k > 0) ok = spin_ge(tc_ij, k, a.err);
-      ok = ok && spin_ge(&a.Rc[(size_t)k * NG + 0], need, a.err);
+    FST(7);
+    S* Xt = ts ? A + (size_t)j * B * ldm + (size_t)i * B : At;
+    if (active) load_strip_pair<B, S>(X, Xt, ldm, col);
+    if (!dma_next) {
+      DmaJob<B> d{lds + buf * BUF, flow_vw<B>(a, i, k, 0), flow_tw<B>(a, i, k, 0), true};
+      for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
     }
-    if (!wg_acquire(ok, sflag)) return;
-    S* Bt = A + (size_t)j * B * ldm + (size_t)i * B;
-    const S* Vt = A + (size_t)k * B * ldm + (size_t)i * B;
-    if (active) load_strip<B>(X, Bt, ldm, col, 0);
-    group_load<B, false>(R, Vt, ldm, 0, flow_tw<B>(a, i, k, 0));
+    dma_next = false;
+    // head rows: written by another workgroup before this segment (sc1 loads) or by this one
+    if (ts && active) {
+      if (i == ifirst || i == k + 1) load_head<B, S, true>(H, At, ldm, 0, col);
+      else load_head<B, S, false>(H, At, ldm, 0, col);
+    }
+    FST(4);
+    const int inext = (i == k) ? i0 : i + 1;
+    const bool has_next = inext < i1;
     for (int g = 0; g < NG; ++g) {
-      group_commit<B, false>(R, Vb(buf), Tb(buf), g * IB);
-      __syncthreads();
+      {
+        bool ok = true;
+        if (t == 0) {
+          if (g + 1 < NG) ok = pv.ensure(rc, g + 1, need, a.err);
+          else if (has_next) ok = pv.ensure(rc, 0, inext - k + 1, a.err);
+        }
+        FST(0);
+        if (!sync_point<true>(ok, sflag, par)) return;
+      }
+      if (g == 0 && pending) {
+        publish_after_drain(pending, 1);
+        pending = nullptr;
+      }
+      FST(7);
+      const double* Vs = lds + buf * BUF;
+      const double* Ts = Vs + G::VIMG;
+      // the other buffer is free (every wave passed this sync point): next DMA rides phase 1
+      DmaJob<B> d{lds + (buf ^ 1) * BUF, nullptr, nullptr, false};
       if (g + 1 < NG) {
-        const bool okg = t == 0 ? spin_ge(&a.Rc[(size_t)k * NG + g + 1], need, a.err) : true;
-        if (!wg_acquire(okg, sflag)) return;
-        group_load<B, false>(R, Vt, ldm, (g + 1) * IB, flow_tw<B>(a, i, k, g + 1));
+        d.v = flow_vw<B>(a, i, k, g + 1);
+        d.t = flow_tw<B>(a, i, k, g + 1);
+        d.on = true;
+      } else if (has_next) {
+        d.v = flow_vw<B>(a, inext, k, 0);
+        d.t = flow_tw<B>(a, inext, k, 0);
+        d.on = true;
+        dma_next = true;
       }
       if (active) {
-        load_head<B>(H, At, ldm, g * IB, col);
-        apply_group<B, true>(Vb(buf), Tb(buf), X, H, 0);
-        store_head<B>(H, At, ldm, g * IB, col);
+        if (ts) apply_zw<B, true>(Vs, Ts, X, H, W, 0, d);
+        else apply_zw<B, false>(Vs, Ts, X, H, W, g * IB / 4, d);
+      } else {
+        for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
       }
+      FST(3);
+      if (ts && active) {
+        // head rows stay with this workgroup for the whole segment: plain (write-back) stores,
+        // made visible to the next segment's workgroup by one release before the Ac publish
+        store_head_plain<B>(H, At, ldm, g * IB, col);
+        if (g + 1 < NG) {
+          if (i == ifirst || i == k + 1) load_head<B, S, true>(Hn, At, ldm, (g + 1) * IB, col);
+          else load_head<B, S, false>(Hn, At, ldm, (g + 1) * IB, col);
+        }
+      }
+      FST(2);
+      if (active) {
+        if (ts) apply_x<B, true>(Vs, X, W, 0);
+        else apply_x<B, false>(Vs, X, W, g * IB / 4);
+      }
+      FST(3);
+#pragma unroll
+      for (int r = 0; r < G::NRI; ++r) H[r] = Hn[r];
       buf ^= 1;
     }
-    if (active) store_strip<B>(X, Bt, ldm, col, 0);
-    wg_publish(tc_ij, 1);
+    if (active) store_strip_pair<B, S>(X, Xt, ldm, col);
+    pending = tc(i);
+    FST(4);
   }
-  wg_publish(ac, 1);
+  // last element's strip and the segment: drain, then publish both
+  sync_point<true>(true, sflag, par);
+  if (pending) publish_after_drain(pending, 1);
+  if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the plain-stored head rows
+  publish_after_drain(ac, 1);
+  FST(4);
 }
 
 // dynamic LDS (doubles) of the two task paths; two ints follow (task index, wait verdict)
@@ -327,7 +446,7 @@ template <int B>
 constexpr int flow_lds_doubles() {
   using G = Geo<B>;
   constexpr int panel = G::VSZ + 8 * G::TSZ + G::IB + 2 + 2 * 4 * 32 + 4 * 32 + 2 * 32;
-  constexpr int chain = 2 * (G::VSZ + G::TSZ);
+  constexpr int chain = 2 * (G::VIMG + G::TIMG);
   return panel > chain ? panel : chain;
 }
 
@@ -336,6 +455,14 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
   extern __shared__ __align__(16) double lds[];
   int* s_task = reinterpret_cast<int*>(lds + flow_lds_doubles<B>());
   int* s_flag = s_task + 1;
+#ifdef TQR_FLOW_STAMPS
+  if (threadIdx.x == 0) {
+    unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 2);
+    l_[0] = __builtin_amdgcn_s_memrealtime();
+    for (int c = 0; c < 8; ++c) l_[1 + c] = 0;
+  }
+  int* sflag = s_flag;
+#endif
   for (;;) {
     if (threadIdx.x == 0) {
       int idx = __hip_atomic_fetch_add(a.next, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -356,6 +483,13 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
     }
     __syncthreads();
   }
+#ifdef TQR_FLOW_STAMPS
+  FST(6);
+  if (threadIdx.x == 0) {
+    unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 2);
+    for (int c = 0; c < 8; ++c) g_fst[blockIdx.x * 8 + c] = l_[1 + c];
+  }
+#endif
 }
 
 }  // namespace tqr

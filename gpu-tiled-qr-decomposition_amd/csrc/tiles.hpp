@@ -60,12 +60,22 @@ struct Geo {
   static constexpr int TP = IB + 1;           // LDS pitch of T / Gram / head images
   static constexpr int VSZ = B * VP;          // V image (doubles)
   static constexpr int TSZ = IB * TP;         // T image (doubles)
+  // workspace slots / LDS-DMA images, rounded up to whole KiB (128 doubles)
+  static constexpr int VIMG = (VSZ + 127) / 128 * 128;
+  static constexpr int TIMG = (TSZ + 127) / 128 * 128;
   // V image column permutation: the NRI values a lane needs per row are contiguous.
   __device__ static constexpr int pc(int c) { return (c & 3) * NRI + (c >> 2); }
 };
 
 template <typename S>
 __device__ __forceinline__ double ld(const S* p) { return (double)*p; }
+// L1-bypassing (sc1) load: data handed over by another workgroup inside a launch, read without an
+// agent-scope acquire (MI355X_MICROARCH.md, visibility "Valid forms", first table row: every
+// byte stored sc1 and drained before one lane's counter add; every load of it sc1).
+template <typename S>
+__device__ __forceinline__ double ldc(const S* p) {
+  return (double)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // Global stores are write-through (sc1): results are handed to workgroups on other XCDs, and a
 // release fence then has no dirty L2 lines of ours to write back (MI355X_MICROARCH.md,
 // "publish-large").
@@ -96,34 +106,51 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 // part acting on the IB head rows H of the strip); else GE-type (V = unit-lower trapezoid
 // stored explicitly, rows < 4*ks0 are zero and skipped).
 // ---------------------------------------------------------------------------------------
-template <int B, bool HEAD>
-__device__ __forceinline__ void apply_group(const double* __restrict__ Vs, const double* __restrict__ Ts,
-                                            double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI], int ks0) {
+// Phase 1: Z = [H] + V^T X, W = -T^T Z, H += W (TS). Phase 2: X += V W.
+// hook.step(m) is called once per two k-steps of phase 1 (m = 0, 1, ...) inside the MFMA
+// stream, then for the remaining m < Hook::STEPS after the loop: the chain engine issues the
+// next group's LDS-DMA there (flow.hpp), so its issue cost hides under the MFMAs.
+struct NoHook {
+  __device__ __forceinline__ void step(int) const {}
+  static constexpr int STEPS = 0;
+};
+template <int B, bool HEAD, typename Hook = NoHook>
+__device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const double* __restrict__ Ts,
+                                         const double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI],
+                                         double (&W)[Geo<B>::NRI], int ks0, const Hook& hook = Hook()) {
   using g = Geo<B>;
   constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP, TP = g::TP;
   const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
   double Z[NRI];
 #pragma unroll
   for (int r = 0; r < NRI; ++r) Z[r] = HEAD ? H[r] : 0.0;
-  // Z += V^T X   (A operand: V[4ks+x][4ri+y])
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    // bound the scheduler's hoisting of V-image reads (else it lifts ~500 LDS loads and spills)
-    if ((ks & 3) == 0) asm volatile("" ::: "memory");
-    if (!HEAD && ks < ks0) continue;
+  // Z += V^T X   (A operand: V[4ks+x][4ri+y]); software-pipelined: the LDS reads of k-step
+  // ks+1 are issued ahead of the MFMAs of ks (one wave per SIMD cannot hide LDS latency
+  // otherwise; tools/ubench/apply_bench.hip: 73 % -> 83 % of peak)
+  auto ldz = [&](double (&a)[NRI], int ks) {
     const double2* vr = reinterpret_cast<const double2*>(Vs + (4 * ks + x) * VP + y * NRI);
-    double a[NRI];
 #pragma unroll
     for (int h = 0; h < NRI / 2; ++h) {
-      double2 t = vr[h];
+      const double2 t = vr[h];
       a[2 * h] = t.x;
       a[2 * h + 1] = t.y;
     }
+  };
+  double ac[NRI], an[NRI];
+  ldz(ac, HEAD ? 0 : ks0);
 #pragma unroll
-    for (int r = 0; r < NRI; ++r) Z[r] = mfma4(a[r], X[ks], Z[r]);
+  for (int ks = 0; ks < NKS; ++ks) {
+    asm volatile("" ::: "memory");  // one k-step per region: bounds the hoisting of LDS reads
+    if ((ks & 1) == 0) hook.step(ks / 2);
+    if (!HEAD && ks < ks0) continue;
+    if (ks + 1 < NKS) ldz(an, ks + 1);
+#pragma unroll
+    for (int r = 0; r < NRI; ++r) Z[r] = mfma4(ac[r], X[ks], Z[r]);
+#pragma unroll
+    for (int r = 0; r < NRI; ++r) ac[r] = an[r];
   }
-  // W = T^T Z   (A operand: T[4k2+x][4wi+y]); T upper triangular -> k2 <= wi.
-  double W[NRI];
+  for (int m = NKS / 2; m < Hook::STEPS; ++m) hook.step(m);
+  // W = -T^T Z   (A operand: T[4k2+x][4wi+y]); T upper triangular -> k2 <= wi.
 #pragma unroll
   for (int wi = 0; wi < NRI; ++wi) {
     double acc = 0.0;
@@ -135,38 +162,65 @@ __device__ __forceinline__ void apply_group(const double* __restrict__ Vs, const
 #pragma unroll
     for (int r = 0; r < NRI; ++r) H[r] += W[r];
   }
-  // X -= V W   (A operand: V[4ks+y][4wi+x]); 4 row blocks interleaved to hide MFMA latency.
+}
+
+template <int B, bool HEAD>
+__device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&X)[Geo<B>::NKS],
+                                        const double (&W)[Geo<B>::NRI], int ks0) {
+  using g = Geo<B>;
+  constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP;
+  const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
+  // X += V W   (A operand: V[4ks+y][4wi+x]); two k-steps per region, next pair's reads ahead.
+  auto ldx = [&](double (&a)[NRI], int ks) {
+    const double2* vr = reinterpret_cast<const double2*>(Vs + (4 * ks + y) * VP + x * NRI);
 #pragma unroll
-  for (int kb = 0; kb < NKS; kb += 4) {
+    for (int h = 0; h < NRI / 2; ++h) {
+      const double2 t = vr[h];
+      a[2 * h] = t.x;
+      a[2 * h + 1] = t.y;
+    }
+  };
+  double bc[2][NRI], bn[2][NRI];
+  const int kx = HEAD ? 0 : (ks0 & ~1);
+  ldx(bc[0], kx);
+  ldx(bc[1], kx + 1);
+#pragma unroll
+  for (int kb = 0; kb < NKS; kb += 2) {
     asm volatile("" ::: "memory");
-    if (!HEAD && kb + 3 < ks0) continue;
-    double a[4][NRI];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const double2* vr = reinterpret_cast<const double2*>(Vs + (4 * (kb + u) + y) * VP + x * NRI);
-#pragma unroll
-      for (int h = 0; h < NRI / 2; ++h) {
-        double2 t = vr[h];
-        a[u][2 * h] = t.x;
-        a[u][2 * h + 1] = t.y;
-      }
+    if (!HEAD && kb + 1 < ks0) continue;
+    if (kb + 2 < NKS) {
+      ldx(bn[0], kb + 2);
+      ldx(bn[1], kb + 3);
     }
 #pragma unroll
     for (int wi = 0; wi < NRI; ++wi)
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (HEAD || kb + u >= ks0) X[kb + u] = mfma4(a[u][wi], W[wi], X[kb + u]);
+      for (int u = 0; u < 2; ++u)
+        if (HEAD || kb + u >= ks0) X[kb + u] = mfma4(bc[u][wi], W[wi], X[kb + u]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < NRI; ++r) bc[u][r] = bn[u][r];
   }
 }
 
+template <int B, bool HEAD>
+__device__ __forceinline__ void apply_group(const double* __restrict__ Vs, const double* __restrict__ Ts,
+                                            double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI], int ks0) {
+  double W[Geo<B>::NRI];
+  apply_zw<B, HEAD>(Vs, Ts, X, H, W, ks0);
+  apply_x<B, HEAD>(Vs, X, W, ks0);
+}
+
 // Strip loads/stores: X[ks] <- tile(rows 4ks+x, column col0 + 4blk + y).
-template <int B, typename S>
+// SC1: L1-bypassing loads (data another workgroup of the same launch stored, see ldc)
+template <int B, typename S, bool SC1 = false>
 __device__ __forceinline__ void load_strip(double (&X)[Geo<B>::NKS], const S* __restrict__ tile, size_t ldm,
                                            int col0, int ks0) {
   const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
   const S* p = tile + (size_t)c * ldm + x;
 #pragma unroll
-  for (int ks = 0; ks < Geo<B>::NKS; ++ks) X[ks] = ks >= ks0 ? ld(p + 4 * ks) : 0.0;
+  for (int ks = 0; ks < Geo<B>::NKS; ++ks) X[ks] = ks >= ks0 ? (SC1 ? ldc(p + 4 * ks) : ld(p + 4 * ks)) : 0.0;
 }
 template <int B, typename S>
 __device__ __forceinline__ void store_strip(const double (&X)[Geo<B>::NKS], S* __restrict__ tile, size_t ldm,
@@ -178,13 +232,65 @@ __device__ __forceinline__ void store_strip(const double (&X)[Geo<B>::NKS], S* _
     if (ks >= ks0) st(p + 4 * ks, X[ks]);
 }
 // Head rows of group g: H[ri] <- tile(row r0 + 4ri + x, column col0 + 4blk + y).
-template <int B, typename S>
+template <int B, typename S, bool SC1 = false>
 __device__ __forceinline__ void load_head(double (&H)[Geo<B>::NRI], const S* __restrict__ tile, size_t ldm,
                                           int r0, int col0) {
   const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
   const S* p = tile + (size_t)c * ldm + r0 + x;
 #pragma unroll
-  for (int r = 0; r < Geo<B>::NRI; ++r) H[r] = ld(p + 4 * r);
+  for (int r = 0; r < Geo<B>::NRI; ++r) H[r] = SC1 ? ldc(p + 4 * r) : ld(p + 4 * r);
+}
+
+// Chain strips in the paired row map: X[2h + e] at lane x <-> tile row 8h + 2x + e, so a lane
+// moves two consecutive rows of its column per (16-B for fp64) access. The chain's V images are
+// stored with their rows permuted to match (vimg_row). Loads and stores are sc1 buffer accesses
+// (L1-bypassing / write-through: inter-workgroup hand-off without acquire/release fences).
+// buffer descriptor over a wave-uniform base: readfirstlane makes the uniformity provable, else
+// hipcc wraps every buffer access in a waterfall loop (cdna_hip_programming.md T20)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
+  const unsigned long long u = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ int vimg_row(int q) { return 8 * (q >> 3) + 2 * (q & 3) + ((q >> 2) & 1); }
+template <int B, typename S>
+__device__ __forceinline__ void load_strip_pair(double (&X)[Geo<B>::NKS], S* tile, size_t ldm, int col0) {
+  const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
+  __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile);
+  const unsigned base = (unsigned)(((size_t)c * ldm + 2 * x) * sizeof(S));
+#pragma unroll
+  for (int h = 0; h < Geo<B>::NKS / 2; ++h) {
+    const unsigned off = base + 8 * h * sizeof(S);
+    if constexpr (sizeof(S) == 8) {
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+      X[2 * h] = __longlong_as_double(((long long)v[1] << 32) | v[0]);
+      X[2 * h + 1] = __longlong_as_double(((long long)v[3] << 32) | v[2]);
+    } else {
+      auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 16);
+      X[2 * h] = (double)__uint_as_float(v[0]);
+      X[2 * h + 1] = (double)__uint_as_float(v[1]);
+    }
+  }
+}
+template <int B, typename S>
+__device__ __forceinline__ void store_strip_pair(const double (&X)[Geo<B>::NKS], S* tile, size_t ldm, int col0) {
+  const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
+  __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile);
+  const unsigned base = (unsigned)(((size_t)c * ldm + 2 * x) * sizeof(S));
+#pragma unroll
+  for (int h = 0; h < Geo<B>::NKS / 2; ++h) {
+    const unsigned off = base + 8 * h * sizeof(S);
+    if constexpr (sizeof(S) == 8) {
+      const unsigned long long a = (unsigned long long)__double_as_longlong(X[2 * h]);
+      const unsigned long long b = (unsigned long long)__double_as_longlong(X[2 * h + 1]);
+      __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);
+    } else {
+      __attribute__((ext_vector_type(2))) unsigned v = {__float_as_uint((float)X[2 * h]), __float_as_uint((float)X[2 * h + 1])};
+      __builtin_amdgcn_raw_buffer_store_b64(v, rs, off, 0, 16);
+    }
+  }
 }
 template <int B, typename S>
 __device__ __forceinline__ void store_head(const double (&H)[Geo<B>::NRI], S* __restrict__ tile, size_t ldm,
@@ -193,6 +299,14 @@ __device__ __forceinline__ void store_head(const double (&H)[Geo<B>::NRI], S* __
   S* p = tile + (size_t)c * ldm + r0 + x;
 #pragma unroll
   for (int r = 0; r < Geo<B>::NRI; ++r) st(p + 4 * r, H[r]);
+}
+template <int B, typename S>
+__device__ __forceinline__ void store_head_plain(const double (&H)[Geo<B>::NRI], S* __restrict__ tile, size_t ldm,
+                                                 int r0, int col0) {
+  const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
+  S* p = tile + (size_t)c * ldm + r0 + x;
+#pragma unroll
+  for (int r = 0; r < Geo<B>::NRI; ++r) p[4 * r] = (S)H[r];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -218,13 +332,12 @@ __device__ __forceinline__ void stage_v_ge(double* Vs, const S* __restrict__ vt,
     Vs[r * g::VP + g::pc(c)] = r < d ? 0.0 : (r == d ? 1.0 : ld(vt + (size_t)d * ldm + r));
   }
 }
+// T workspace slot (Tw): the T image itself, T[r][c] at r * TP + c, padded to whole KiB so the
+// chain engine copies it verbatim by LDS-DMA.
 template <int B>
 __device__ __forceinline__ void stage_t(double* Ts, const double* __restrict__ tg) {
   using g = Geo<B>;
-  for (int idx = threadIdx.x; idx < g::IB * g::IB; idx += NT) {
-    int r = idx / g::IB, c = idx % g::IB;
-    Ts[r * g::TP + c] = tg[idx];
-  }
+  for (int idx = threadIdx.x; idx < g::IB * g::TP; idx += NT) Ts[idx] = tg[idx];
 }
 
 // ---------------------------------------------------------------------------------------

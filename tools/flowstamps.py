@@ -1,0 +1,31 @@
+"""Diagnostic: activity breakdown of the persistent engine k_flow (libtqr_fst.so, per-workgroup
+s_memrealtime sums, flow.hpp FST categories). Usage: python tools/flowstamps.py [m] [n] [b]"""
+import ctypes, os, sys, time
+import torch
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpu-tiled-qr-decomposition_amd"))
+import tqr
+tqr.LIB_PATH = tqr.LIB_PATH.replace("libtqr.so", "libtqr_fst.so")
+L = tqr.lib()
+m = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+n = int(sys.argv[2]) if len(sys.argv) > 2 else m
+b = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+A = torch.empty((n, m), dtype=torch.float64, device="cuda")
+tau = torch.zeros((min(m, n) // b, m), dtype=torch.float64, device="cuda")
+p = tqr.TiledQR(m, n, b, torch.float64)
+for rep in range(2):
+    tqr.fill_randzo(A, m, n, 5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    p.execute(A, tau)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+nb = torch.cuda.get_device_properties(0).multi_processor_count
+st = (ctypes.c_ulonglong * (8 * nb))()
+assert L.tqr_debug_flow_stamps(st, nb) == 0
+names = ["chain polls (thread 0)", "panel waits", "chain head-row I/O", "chain apply (+DMA issue)",
+         "chain strip I/O+publish", "panel compute", "dequeue/dispatch/exit", "chain drain+barrier"]
+tot = [sum(st[w * 8 + c] for w in range(nb)) for c in range(8)]
+allt = sum(tot)
+print(f"{m}x{n} b={b}: wall {ms:.1f} ms; {nb} workgroups; sum of stamps {allt / nb / 1e5:.1f} ms per WG")
+for c in range(8):
+    print(f"  {names[c]:24s} {tot[c] / nb / 1e5:8.2f} ms/WG  {100.0 * tot[c] / allt:5.1f}%")

@@ -1,0 +1,14 @@
+"""Sweep the flow plan's cost model / segment length (env TQR_TG, TQR_SEGLEN) at one size."""
+import os, subprocess, sys, json
+m = sys.argv[1] if len(sys.argv) > 1 else "16384"
+for seg in ["8", "4", "16"]:
+    for tg in ["0.7", "1.0", "1.4", "2.0"]:
+        env = dict(os.environ, TQR_TG=tg, TQR_SEGLEN=seg)
+        r = subprocess.run([sys.executable, "bench.py", "--no-cpu-baseline", "--steps", "3", "--warmup", "1", "--m", m, "--n", m],
+                           env=env, capture_output=True, text=True, timeout=120)
+        try:
+            j = json.loads(r.stdout.strip().splitlines()[-1])
+            print(f"seglen {seg:>3} Tg {tg:>4}: {j['ms_per_step']:8.2f} ms  {j['value']/1e3:6.2f} TF/s", flush=True)
+        except Exception:
+            print("failed", seg, tg, r.stderr[-500:], flush=True)
+            sys.exit(1)
