@@ -9,9 +9,12 @@ qrdecomp.c:1383). A step = restore the input from a resident HBM copy (device-to
 included in the step) + one whole factorisation. GFLOP/s uses the algorithmic count
 2mn^2 - 2n^3/3.
 
-N > 1 (torchrun, one process per GPU): every rank factorises its own 16384^2 matrix
-(replicas — the tile-column-partitioned RCCL path is not in this round), so
-per-GPU work is fixed ("scaling": "weak") and value = all ranks' flops / max-over-ranks time.
+N > 1 (torchrun, one process per GPU): ONE matrix, BASELINE.json configs[3] by default
+(65536 x 16384 fp64, tile 256), factorised by all ranks together — tile column j on rank
+j % N, the owner of each panel forwarding its reflector groups' V/T images to the peers over
+xGMI inside the persistent launch (DESIGN.md §7). Total work is fixed ("scaling": "strong");
+value = the matrix's algorithmic flops / max-over-ranks time. Each step restores the rank's
+own tile columns from a resident copy, resets its counters, barriers, and factorises.
 
 Extra objects on the line:
   roofline      — the dominant kernel (trailing-update: TSMQR/UNMQR strips on
@@ -101,9 +104,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--m", type=int, default=16384)
-    ap.add_argument("--n", type=int, default=16384)
-    ap.add_argument("--b", type=int, default=256)
+    # (no --m/--n: torch.distributed.run's parser would claim them as abbreviations)
+    ap.add_argument("--rows", type=int, default=None, help="m (default 16384 at N=1, 65536 at N>1)")
+    ap.add_argument("--cols", type=int, default=None, help="n (default 16384)")
+    ap.add_argument("--tile", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=6144)
     args = ap.parse_args()
@@ -115,22 +119,35 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # TQR_BENCH_DEVICE / TQR_BENCH_BACKEND: rehearse N > 1 with all ranks on one GPU over gloo
+    dev = int(os.environ.get("TQR_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
-    torch.cuda.set_device(local_rank)
-    m, n, b = args.m, args.n, args.b
+        backend = os.environ.get("TQR_BENCH_BACKEND", "nccl")  # nccl = RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+    m = args.rows or (16384 if world == 1 else 65536)
+    n = args.cols or 16384
+    b = args.tile
     dt = torch.float64
+    q = n // b
 
     A0 = torch.empty((n, m), dtype=dt, device="cuda")
-    tqr.fill_randzo(A0, m, n, 5 + rank)
+    tqr.fill_randzo(A0, m, n, 5)
     A = torch.empty_like(A0)
+    A.copy_(A0)
     tau = torch.zeros((min(m, n) // b, m), dtype=dt, device="cuda")
-    plan = tqr.TiledQR(m, n, b, dt)
+    plan = tqr.TiledQR(m, n, b, dt) if world == 1 else tqr.DistTiledQR(m, n, b, dt)
     stream = torch.cuda.current_stream().cuda_stream
+    # this rank's tile columns (all of them at N = 1): rows j*b..j*b+b-1 of the (n, m) array
+    own_A = A.view(q, b, m)[rank::world]
+    own_A0 = A0.view(q, b, m)[rank::world]
 
     def step():
-        A.copy_(A0)
+        own_A.copy_(own_A0)
         plan.execute(A, tau, stream=stream)
 
     for _ in range(args.warmup):
@@ -148,26 +165,29 @@ def main():
     t1 = time.perf_counter()
     el = t1 - t0
     if dist:
-        tt = torch.tensor([el], dtype=torch.float64)
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+    if hasattr(plan, "status"):
+        plan.status(stream)
     ms_step = el / args.steps * 1e3
-    total_flops = qr_flops(m, n) * world * args.steps
+    total_flops = qr_flops(m, n) * args.steps
     value = total_flops / el / 1e9
 
     # profiled pass (outside the timed region): per-launch device time of the dominant kernel
     plan.set_profile(True)
-    A.copy_(A0)
+    own_A.copy_(own_A0)
     plan.execute(A, tau, stream=stream)
     torch.cuda.synchronize()
     st = plan.stats()
     plan.set_profile(False)
     uf = update_flops(m, n, b)
-    achieved = uf / (st["ms_update"] * 1e-3) / 1e12 if st["ms_update"] > 0 else None
+    # per GPU: its share of the update flops (1/N of the job at N > 1) over its launch time
+    achieved = uf / world / (st["ms_update"] * 1e-3) / 1e12 if st["ms_update"] > 0 else None
     traffic = load_traffic(m, n, b)
     roof = {
         "bound": "mfma",
-        "kernel": "k_update (TSMQR/UNMQR strips, v_mfma_f64_4x4x4_4b_f64)",
+        "kernel": "k_flow (persistent engine; TSMQR/UNMQR strips on v_mfma_f64_4x4x4_4b_f64)",
         "achieved": round(achieved, 3) if achieved else None,
         "peak": FP64_MFMA_PEAK_TFLOPS,
         "unit": "TFLOP/s",
@@ -183,6 +203,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample, b)
 
+    cfg = 2 if (m, n) == (16384, 16384) else 3 if (m, n) == (65536, 16384) else 1 if (m, n) == (4096, 4096) else "custom"
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -193,12 +214,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (RANDZO distribution, device-generated)",
-            "config": {"workload": f"tiled QR {m}x{n} fp64, tile {b} (BASELINE configs[2])", "m": m, "n": n,
-                       "tile": b, "parallelism": "single GPU" if world == 1 else f"{world} replicas"},
+            "config": {"workload": f"tiled QR {m}x{n} fp64, tile {b} (BASELINE configs[{cfg}])", "m": m, "n": n,
+                       "tile": b, "parallelism": "single GPU" if world == 1 else
+                       f"{world} GPUs, tile-column cyclic, panel V/T forwarded over xGMI"},
             "roofline": roof,
             "cpu_baseline": cpu,
         }

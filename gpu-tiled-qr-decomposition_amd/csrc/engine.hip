@@ -466,6 +466,24 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
     for (auto& t : tl) fp.items.push_back(t.it);
   }
 }
+// Multi-GPU: keep this rank's share of the global (topological) order — panel tasks of the tile
+// columns it owns (column k on rank k % world) each followed by the forward task of that panel
+// member, and the chain tasks of its own tile columns. Every rank's list is the global order
+// restricted (FWD(i,k) sits right after QRD(i,k)), so the earliest unfinished task of the whole
+// job can always progress: the multi-rank engine is deadlock-free like the single-GPU one.
+static void partition_flow_plan(FlowPlan& fp, int rank, int world) {
+  std::vector<Item> mine;
+  for (const Item& it : fp.items) {
+    const int ty = it.ts & 0xff;
+    if (ty == T_CHAIN) {
+      if (it.m % world == rank) mine.push_back(it);
+    } else if (it.k % world == rank) {  // QRS(k,k) / QRD(l,k): tile column k
+      mine.push_back(it);
+      mine.push_back(Item{T_FWD, it.l, it.k, it.k});
+    }
+  }
+  fp.items.swap(mine);
+}
 static size_t lds_build_t(int b) {
   int ib = b < 32 ? b : 32;
   return ((size_t)b * (ib + 2) + 6 * (size_t)ib * (ib + 1) + ib + 2) * sizeof(double);
@@ -496,6 +514,11 @@ static size_t vimg_doubles(int b) {
   const size_t ib = b < 32 ? b : 32;
   return ((size_t)b * (ib + 2) + 127) / 128 * 128;
 }
+// flow engine workspace of one step with `rows` tile rows (flow.hpp flow_vw_off / flow_tw_off)
+static size_t wk_bytes(int b, int rows) {
+  const size_t ng = b / (b < 32 ? b : 32);
+  return (size_t)rows * ng * (vimg_doubles(b) + timg_doubles(b)) * sizeof(double);
+}
 
 }  // namespace tqr
 
@@ -507,8 +530,9 @@ struct tqr_plan {
   std::vector<long> off_p, off_u;  // per wave offsets into the item arrays
   Item* d_items_p = nullptr;
   Item* d_items_u = nullptr;
-  double* d_T = nullptr;
-  double* d_V = nullptr;   // V images (flow engine)
+  double* d_T = nullptr;   // T factors of the wave-batched engine
+  std::vector<double*> wk;  // flow engine: per-step panel workspaces (V and T images)
+  double** d_wk = nullptr;  // device table of wk
   hipStream_t sP = nullptr, sU = nullptr;
   hipEvent_t evP = nullptr, evU = nullptr, evStart = nullptr;
   kfn kp = nullptr, ku = nullptr;
@@ -528,6 +552,14 @@ struct tqr_plan {
   std::vector<int> prof_kind;
   int nl_u = 0, nl_p = 0;
   double ms_u = 0, ms_p = 0;
+  // multi-GPU (tile-column cyclic partition): rank / world, uncached panel counters, forward
+  // counters, peer workspaces opened by IPC
+  int rank = 0, world = 1;
+  int* d_rc = nullptr;
+  int* d_fc = nullptr;
+  PeerBufs* d_peers = nullptr;
+  double** d_peer_wk = nullptr;  // world x kmax opened peer workspace pointers
+  std::vector<void*> opened;     // IPC-opened peer pointers
 };
 
 #define HIPCHK(x)                                                                         \
@@ -577,7 +609,8 @@ void tqr_plan_destroy(tqr_plan* pl) {
   if (pl->d_items_p) (void)hipFree(pl->d_items_p);
   if (pl->d_items_u) (void)hipFree(pl->d_items_u);
   if (pl->d_T) (void)hipFree(pl->d_T);
-  if (pl->d_V) (void)hipFree(pl->d_V);
+  for (double* w : pl->wk) (void)hipFree(w);
+  if (pl->d_wk) (void)hipFree(pl->d_wk);
   if (pl->sP) (void)hipStreamDestroy(pl->sP);
   if (pl->sU) (void)hipStreamDestroy(pl->sU);
   if (pl->evP) (void)hipEventDestroy(pl->evP);
@@ -588,10 +621,21 @@ void tqr_plan_destroy(tqr_plan* pl) {
   if (pl->ev0) (void)hipEventDestroy(pl->ev0);
   if (pl->ev1) (void)hipEventDestroy(pl->ev1);
   for (auto e : pl->prof_ev) (void)hipEventDestroy(e);
+  for (void* p : pl->opened) (void)hipIpcCloseMemHandle(p);
+  if (pl->d_peers) (void)hipFree(pl->d_peers);
+  if (pl->d_peer_wk) (void)hipFree(pl->d_peer_wk);
+  if (pl->d_rc) (void)hipFree(pl->d_rc);
+  if (pl->d_fc) (void)hipFree(pl->d_fc);
   delete pl;
 }
 
-int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) {
+static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world);
+int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) { return plan_create(out, m, n, b, dtype, 0, 1); }
+int tqr_dist_plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world) {
+  if (world < 1 || rank < 0 || rank >= world) return TQR_EINVAL;
+  return plan_create(out, m, n, b, dtype, rank, world);
+}
+static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world) {
   if (!out) return TQR_EINVAL;
   *out = nullptr;
   if (!valid_b(b) || m <= 0 || n <= 0 || m % b || n % b || (dtype != TQR_F32 && dtype != TQR_F64))
@@ -601,6 +645,7 @@ int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) {
   tqr_plan* pl = new (std::nothrow) tqr_plan();
   if (!pl) return TQR_ENOMEM;
   pl->m = m; pl->n = n; pl->b = b; pl->p = m / b; pl->q = n / b;
+  pl->rank = rank; pl->world = world;
   pl->kmax = std::min(pl->p, pl->q);
   pl->dtype = dtype;
   pl->es = dtype == TQR_F64 ? 8 : 4;
@@ -629,7 +674,9 @@ int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) {
   tqr_sched_plan_free(&sp);
 
   int ib = b < 32 ? b : 32;
-  size_t tw = (size_t)pl->p * pl->kmax * (b / ib) * timg_doubles(b) * sizeof(double);
+  const char* eng = getenv("TQR_ENGINE");
+  pl->engine = (eng && strcmp(eng, "waves") == 0 && world == 1) ? 0 : 1;
+  size_t tw = pl->engine == 0 ? (size_t)pl->p * pl->kmax * (b / ib) * timg_doubles(b) * sizeof(double) : 8;
   if (hipMalloc(&pl->d_items_p, std::max<size_t>(1, ip.size()) * sizeof(Item)) != hipSuccess ||
       hipMalloc(&pl->d_items_u, std::max<size_t>(1, iu.size()) * sizeof(Item)) != hipSuccess ||
       hipMalloc(&pl->d_T, tw) != hipSuccess) {
@@ -653,26 +700,42 @@ int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) {
   if (resolve(b, dtype, &pl->kp, &pl->ku, &kt) != TQR_OK) { tqr_plan_destroy(pl); return TQR_EHIP; }
   pl->ldsP = lds_panel(b);
   pl->ldsU = lds_update(b);
-  // persistent dataflow engine: task list, progress counters, kernel
-  const char* eng = getenv("TQR_ENGINE");
-  pl->engine = (eng && strcmp(eng, "waves") == 0) ? 0 : 1;
+  // persistent dataflow engine: task list, progress counters, panel workspaces, kernel
   pl->ns = (b + 63) / 64;
   pl->ng = b / ib;
   {
     FlowPlan fp;
     const char* sl = getenv("TQR_SEGLEN");
     build_flow_plan(pl->p, pl->q, b, sl ? std::max(1, atoi(sl)) : 8, fp);
+    if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
     pl->sync_ints = 2 + (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns + (size_t)pl->kmax * pl->q * pl->ns;
-    const size_t vw = (size_t)pl->p * pl->kmax * pl->ng * vimg_doubles(b) * sizeof(double);
     if (pl->nflow <= 0 || hipMalloc(&pl->d_flow, sizeof(Item) * pl->nflow) != hipSuccess ||
-        hipMalloc(&pl->d_V, vw) != hipSuccess ||
-        hipMalloc(&pl->d_sync, sizeof(int) * pl->sync_ints) != hipSuccess) {
+        hipMalloc(&pl->d_sync, sizeof(int) * pl->sync_ints) != hipSuccess ||
+        hipMalloc(&pl->d_wk, sizeof(double*) * pl->kmax) != hipSuccess) {
       tqr_plan_destroy(pl); return TQR_ENOMEM;
+    }
+    // one workspace per step k: V then T images of tiles (k..p-1, k), every group
+    for (int k = 0; k < pl->kmax; ++k) {
+      double* w = nullptr;
+      if (hipMalloc(&w, wk_bytes(b, pl->p - k)) != hipSuccess) { tqr_plan_destroy(pl); return TQR_ENOMEM; }
+      pl->wk.push_back(w);
+    }
+    if (hipMemcpy(pl->d_wk, pl->wk.data(), sizeof(double*) * pl->kmax, hipMemcpyHostToDevice) != hipSuccess) {
+      tqr_plan_destroy(pl); return TQR_EHIP;
     }
     if (hipMemcpy(pl->d_flow, fp.items.data(), sizeof(Item) * pl->nflow, hipMemcpyHostToDevice) != hipSuccess) {
       tqr_plan_destroy(pl); return TQR_EHIP;
+    }
+    if (world > 1) {
+      // panel counters in uncached memory (peers' forward tasks add to them over xGMI)
+      const size_t nrc = sizeof(int) * (size_t)pl->kmax * pl->ng;
+      if (hipExtMallocWithFlags((void**)&pl->d_rc, nrc, hipDeviceMallocUncached) != hipSuccess ||
+          hipMalloc(&pl->d_fc, nrc) != hipSuccess || hipMalloc(&pl->d_peers, sizeof(PeerBufs) * world) != hipSuccess ||
+          hipMalloc(&pl->d_peer_wk, sizeof(double*) * (size_t)world * pl->kmax) != hipSuccess) {
+        tqr_plan_destroy(pl); return TQR_ENOMEM;
+      }
     }
     pl->kflow = resolve_flow(b, dtype);
     pl->ldsF = lds_flow(b);
@@ -701,6 +764,79 @@ int tqr_plan_status(tqr_plan* pl, void* stream) {
   if (err) {
     fprintf(stderr, "tqr: dataflow engine aborted (error word %d: a dependency wait timed out)\n", err);
     return TQR_EHIP;
+  }
+  return TQR_OK;
+}
+
+// ---- multi-GPU ------------------------------------------------------------------------------
+size_t tqr_dist_handle_bytes(const tqr_plan* pl) {
+  return pl ? sizeof(hipIpcMemHandle_t) * (1 + (size_t)pl->kmax) : 0;
+}
+
+int tqr_dist_export(tqr_plan* pl, void* buf, size_t len) {
+  if (!pl || pl->world < 2 || !buf || len < tqr_dist_handle_bytes(pl)) return TQR_EINVAL;
+  std::vector<hipIpcMemHandle_t> h(1 + pl->kmax);
+  HIPCHK(hipIpcGetMemHandle(&h[0], pl->d_rc));
+  for (int k = 0; k < pl->kmax; ++k) HIPCHK(hipIpcGetMemHandle(&h[1 + k], pl->wk[k]));
+  memcpy(buf, h.data(), sizeof(hipIpcMemHandle_t) * h.size());
+  return TQR_OK;
+}
+
+int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
+  const size_t hb = tqr_dist_handle_bytes(pl);
+  if (!pl || pl->world < 2 || !all || len < (size_t)pl->world * hb || !pl->opened.empty()) return TQR_EINVAL;
+  std::vector<PeerBufs> pb(pl->world);
+  std::vector<double*> pwk((size_t)pl->world * pl->kmax, nullptr);
+  for (int r = 0; r < pl->world; ++r) {
+    double** tab = pl->d_peer_wk + (size_t)r * pl->kmax;
+    if (r == pl->rank) {
+      for (int k = 0; k < pl->kmax; ++k) pwk[(size_t)r * pl->kmax + k] = pl->wk[k];
+      pb[r] = PeerBufs{tab, pl->d_rc};
+      continue;
+    }
+    std::vector<hipIpcMemHandle_t> h(1 + pl->kmax);
+    memcpy(h.data(), (const char*)all + (size_t)r * hb, hb);
+    void* p = nullptr;
+    for (int x = 0; x <= pl->kmax; ++x) {
+      if (hipIpcOpenMemHandle(&p, h[x], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+        fprintf(stderr, "tqr: rank %d cannot open rank %d's workspace (IPC handle %d)\n", pl->rank, r, x);
+        return TQR_EHIP;
+      }
+      pl->opened.push_back(p);
+      if (x == 0) pb[r].Rc = (int*)p;
+      else pwk[(size_t)r * pl->kmax + x - 1] = (double*)p;
+    }
+    pb[r].Wk = tab;
+  }
+  HIPCHK(hipMemcpy(pl->d_peer_wk, pwk.data(), sizeof(double*) * pwk.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(pl->d_peers, pb.data(), sizeof(PeerBufs) * pl->world, hipMemcpyHostToDevice));
+  return TQR_OK;
+}
+
+int tqr_dist_reset(tqr_plan* pl, void* stream) {
+  if (!pl || pl->world < 2) return TQR_EINVAL;
+  hipStream_t cs = (hipStream_t)stream;
+  HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
+  HIPCHK(hipMemsetAsync(pl->d_rc, 0, sizeof(int) * (size_t)pl->kmax * pl->ng, cs));
+  HIPCHK(hipMemsetAsync(pl->d_fc, 0, sizeof(int) * (size_t)pl->kmax * pl->ng, cs));
+  return TQR_OK;
+}
+
+int tqr_dist_owner(const tqr_plan* pl, int tile_col) {
+  if (!pl || tile_col < 0 || tile_col >= pl->q) return TQR_EINVAL;
+  return tile_col % pl->world;
+}
+
+int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd) {
+  if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1 || world < 1 || rank < 0 || rank >= world) return TQR_EINVAL;
+  FlowPlan fp;
+  build_flow_plan(M, N, b, seglen, fp);
+  if (world > 1) partition_flow_plan(fp, rank, world);
+  if (ntasks) *ntasks = (int)fp.items.size();
+  if (nfwd) {
+    int c = 0;
+    for (auto& it : fp.items) c += (it.ts & 0xff) == T_FWD;
+    *nfwd = c;
   }
   return TQR_OK;
 }
@@ -744,12 +880,14 @@ int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream)
   if (pl->engine == 1) {
     if (!pl->kflow || !pl->d_flow || !pl->d_sync) return TQR_EINVAL;
     FlowArgs f;
-    f.A = dA; f.tau = dtau; f.Tw = pl->d_T; f.Vw = pl->d_V; f.tasks = pl->d_flow; f.ntasks = pl->nflow; f.ldm = ldda;
+    f.A = dA; f.tau = dtau; f.Wk = pl->d_wk; f.tasks = pl->d_flow; f.ntasks = pl->nflow; f.ldm = ldda;
     f.m = pl->m; f.p = pl->p; f.q = pl->q; f.kmax = pl->kmax; f.ns = pl->ns;
     f.next = pl->d_sync; f.err = pl->d_sync + 1; f.Rc = pl->d_sync + 2;
     f.Tc = f.Rc + (size_t)pl->kmax * pl->ng;
     f.Ac = f.Tc + (size_t)pl->p * pl->q * pl->ns;
-    HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
+    f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.peers = pl->d_peers; f.Fc = pl->d_fc;
+    if (pl->world > 1) f.Rc = pl->d_rc;  // counters reset by tqr_dist_reset (all ranks, then a barrier)
+    else HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
     if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
     hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(FLOW_NT), pl->ldsF, cs, f);
     HIPCHK(hipGetLastError());

@@ -24,6 +24,7 @@
 namespace tqr {
 
 constexpr int T_CHAIN = 4;
+constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel member to every peer
 
 // Diagnostic build only (make flowstamps): per-workgroup s_memrealtime sums by activity.
 // Every FST(c) charges the time since the previous stamp to category c (LDS-resident sums,
@@ -47,11 +48,18 @@ extern __device__ unsigned long long g_fst[];
 constexpr int FLOW_NT = 256;
 constexpr unsigned long long FLOW_TIMEOUT = 500000000ull;  // 5 s of s_memrealtime (100 MHz)
 
+// Multi-GPU (tile-column cyclic partition, one process per GPU): peer buffers opened by IPC.
+struct PeerBufs {
+  double* const* Wk;  // the peer's panel workspaces (IPC-opened into this process), one per k
+  int* Rc;
+};
+
 struct FlowArgs {
   void* A;
   void* tau;
-  double* Tw;      // T images, one Geo<B>::TIMG slot per (tile, group)
-  double* Vw;      // V images (the chain's LDS image of each group), one Geo<B>::VIMG slot
+  // panel workspaces, one allocation per step k (each under the 2 GiB a single IPC export
+  // handles): V images of (i, k, g) for i = k..p-1 (Geo<B>::VIMG slots), then T images (TIMG)
+  double* const* Wk;
   const Item* tasks;
   int ntasks;
   long ldm;
@@ -61,16 +69,25 @@ struct FlowArgs {
   int* Rc;
   int* Tc;
   int* Ac;
+  // multi-GPU: dist = world > 1. Rc then lives in uncached memory written by peers' forward
+  // tasks over xGMI and is accessed at system scope; Fc[k][g] orders this rank's forwards.
+  int dist, rank, world;
+  const PeerBufs* peers;
+  int* Fc;
 };
 
 // ---- synchronisation ---------------------------------------------------------------------
 __device__ __forceinline__ int ld_relaxed(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-// thread 0 only: spin until *p >= target; false on error / timeout
-__device__ __noinline__ bool spin_ge(int* p, int target, int* err) {
-  if (ld_relaxed(p) >= target) return true;
+__device__ __forceinline__ int ld_sys(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+__device__ __forceinline__ int ld_cnt(int* p, bool sys) { return sys ? ld_sys(p) : ld_relaxed(p); }
+
+// thread 0 only: spin until *p >= target; false on error / timeout. sys: the counter is written
+// by other devices (system-scope polls)
+__device__ __noinline__ bool spin_ge(int* p, int target, int* err, bool sys = false) {
+  if (ld_cnt(p, sys) >= target) return true;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  while (ld_relaxed(p) < target) {
+  while (ld_cnt(p, sys) < target) {
     if (ld_relaxed(err)) return false;
     __builtin_amdgcn_s_sleep(8);
     if (__builtin_amdgcn_s_memrealtime() - t0 > FLOW_TIMEOUT) {
@@ -86,8 +103,7 @@ __device__ __noinline__ bool spin_ge(int* p, int target, int* err) {
 // (vmcnt(0)) before a workgroup barrier, after which ONE lane bumps the counter (agent atomic);
 // a consumer's thread 0 polls the counter relaxed, a barrier follows, and the other waves read the
 // bytes with sc1 loads — no release / acquire fences (each ~1.7 us at one workgroup per CU).
-// The one exception is the chain's LDS-DMA of V/T images (not a register load): those are read
-// behind an agent-scope acquire, taken once per new observation of the panel counters.
+// The chain's LDS-DMA of V/T images reads write-once data (see PanelView) and needs neither.
 
 // all threads: thread 0's verdict (after its polls)
 __device__ __forceinline__ bool wg_verdict(bool ok0, int* sflag) {
@@ -98,22 +114,34 @@ __device__ __forceinline__ bool wg_verdict(bool ok0, int* sflag) {
   return ok;
 }
 
-// all threads: every wave's (sc1) stores drained, then thread 0 bumps the counter
-__device__ __forceinline__ void wg_publish(int* p, int delta) {
+// all threads: every wave's (sc1) stores drained, then thread 0 bumps the counter (system
+// scope when the counter is also polled by peers' ... / lives in uncached memory)
+__device__ __forceinline__ void wg_publish(int* p, int delta, bool sys = false) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(p, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    if (sys) __hip_atomic_fetch_add(p, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_fetch_add(p, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <int B>
-__device__ __forceinline__ double* flow_tw(const FlowArgs& a, int i, int k, int g) {
+__device__ __forceinline__ size_t flow_vw_off(int p, int i, int k, int g) {
   using G = Geo<B>;
-  return a.Tw + (((size_t)k * a.p + i) * G::NG + g) * G::TIMG;
+  return ((size_t)(i - k) * G::NG + g) * G::VIMG;
+}
+template <int B>
+__device__ __forceinline__ size_t flow_tw_off(int p, int i, int k, int g) {
+  using G = Geo<B>;
+  return (size_t)(p - k) * G::NG * G::VIMG + ((size_t)(i - k) * G::NG + g) * G::TIMG;
+}
+template <int B>
+__device__ __forceinline__ double* flow_tw(const FlowArgs& a, int i, int k, int g) {
+  return a.Wk[k] + flow_tw_off<B>(a.p, i, k, g);
 }
 template <int B>
 __device__ __forceinline__ double* flow_vw(const FlowArgs& a, int i, int k, int g) {
-  using G = Geo<B>;
-  return a.Vw + (((size_t)k * a.p + i) * G::NG + g) * G::VIMG;
+  return a.Wk[k] + flow_vw_off<B>(a.p, i, k, g);
 }
 
 // ---- LDS-DMA staging of one reflector group ------------------------------------------------
@@ -185,16 +213,16 @@ struct PanelView {
     if (threadIdx.x == 0)
       for (int g = 0; g < NG; ++g) rv[g] = 0;
   }
-  __device__ __forceinline__ bool ensure(int* rc, int g, int need, int* err) {
+  __device__ __forceinline__ bool ensure(int* rc, int g, int need, int* err, bool sys) {
     if (rv[g] >= need) return true;
     int v[NG];
 #pragma unroll
-    for (int x = 0; x < NG; ++x) v[x] = ld_relaxed(rc + x);
+    for (int x = 0; x < NG; ++x) v[x] = ld_cnt(rc + x, sys);
 #pragma unroll
     for (int x = 0; x < NG; ++x) rv[x] = v[x];
     if (rv[g] < need) {
-      if (!spin_ge(rc + g, need, err)) return false;
-      rv[g] = ld_relaxed(rc + g);
+      if (!spin_ge(rc + g, need, err, sys)) return false;
+      rv[g] = ld_cnt(rc + g, sys);
     }
     return true;
   }
@@ -235,7 +263,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     const int c0 = g * IB, ks0 = c0 / 4;
     if (!qrs) {  // R_kk rows of group g as left by the previous chain member
       FST(5);
-      const bool ok = t == 0 ? spin_ge(&a.Rc[(size_t)k * NG + g], pos, a.err) : true;
+      const bool ok = t == 0 ? spin_ge(&a.Rc[(size_t)k * NG + g], pos, a.err, a.dist) : true;
       if (!wg_verdict(ok, sflag)) return;
       FST(1);
     }
@@ -306,9 +334,48 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
         store_head<B>(H, Rt, ldm, c0, col);
       }
     }
-    wg_publish(&a.Rc[(size_t)k * NG + g], 1);
+    wg_publish(&a.Rc[(size_t)k * NG + g], 1, a.dist);
   }
   FST(5);
+}
+
+// ---- forward tasks (multi-GPU) -------------------------------------------------------------
+// FWD(i,k) on the owner of panel k: group by group, once member i finished group g here and
+// FWD(i-1,k) forwarded group g (Fc, so every peer counter advances member by member), copy the
+// V and T images of (i,k,g) into every peer's workspace with system-scope (sc0 sc1) 16-B
+// stores over xGMI, drain, release at system scope, and bump each peer's Rc[k][g]. Peers' chains
+// then LDS-DMA the images from their own HBM exactly as the owner's chains do.
+template <int B>
+__device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sflag) {
+  using G = Geo<B>;
+  constexpr int NG = G::NG;
+  const int t = threadIdx.x, pos = i - k;
+  for (int g = 0; g < NG; ++g) {
+    bool ok = true;
+    if (t == 0) ok = spin_ge(&a.Rc[(size_t)k * NG + g], pos + 1, a.err, true) && spin_ge(&a.Fc[(size_t)k * NG + g], pos, a.err);
+    if (!wg_verdict(ok, sflag)) return;
+    const size_t vo = flow_vw_off<B>(a.p, i, k, g), to = flow_tw_off<B>(a.p, i, k, g);
+    const __amdgpu_buffer_rsrc_t vsrc = uniform_rsrc(a.Wk[k] + vo), tsrc = uniform_rsrc(a.Wk[k] + to);
+    for (int r = 0; r < a.world; ++r) {
+      if (r == a.rank) continue;
+      double* pw = a.peers[r].Wk[k];
+      const __amdgpu_buffer_rsrc_t vdst = uniform_rsrc(pw + vo), tdst = uniform_rsrc(pw + to);
+      for (int c = t; c < G::VIMG / 2; c += FLOW_NT)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(vsrc, 16 * c, 0, 16), vdst, 16 * c, 0, 17);
+      for (int c = t; c < G::TIMG / 2; c += FLOW_NT)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(tsrc, 16 * c, 0, 16), tdst, 16 * c, 0, 17);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+      for (int r = 0; r < a.world; ++r)
+        if (r != a.rank) __hip_atomic_fetch_add(&a.peers[r].Rc[(size_t)k * NG + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // peer increments performed before ours
+      __hip_atomic_fetch_add(&a.Fc[(size_t)k * NG + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
 }
 
 // ---- chain tasks ---------------------------------------------------------------------------
@@ -353,7 +420,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
       if (t == 0) {
         if (i == ifirst && seg > 0) ok = spin_ge(ac, seg, a.err);
         if (ok && k > 0) ok = spin_ge(tc(i), k, a.err);
-        if (ok && !dma_next) ok = pv.ensure(rc, 0, need, a.err);
+        if (ok && !dma_next) ok = pv.ensure(rc, 0, need, a.err, a.dist);
       }
       FST(0);
       if (!sync_point<false>(ok, sflag, par)) return;
@@ -378,8 +445,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
       {
         bool ok = true;
         if (t == 0) {
-          if (g + 1 < NG) ok = pv.ensure(rc, g + 1, need, a.err);
-          else if (has_next) ok = pv.ensure(rc, 0, inext - k + 1, a.err);
+          if (g + 1 < NG) ok = pv.ensure(rc, g + 1, need, a.err, a.dist);
+          else if (has_next) ok = pv.ensure(rc, 0, inext - k + 1, a.err, a.dist);
         }
         FST(0);
         if (!sync_point<true>(ok, sflag, par)) return;
@@ -478,6 +545,8 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
     if (type == T_CHAIN) {
       flow_chain<B, S>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                        s_flag);
+    } else if (type == T_FWD) {
+      flow_fwd<B>(a, it.l, it.k, s_flag);
     } else {
       flow_panel<B, S>(a, type, it.l, it.k, lds, s_flag);
     }

@@ -74,6 +74,13 @@ def lib():
     L.tqr_fill_randzo.argtypes = [_I, _P, _I, _I, _I, ctypes.c_ulonglong, _P]
     for nm in ("tqr_tile_geqrt", "tqr_tile_unmqr", "tqr_tile_tsqrt", "tqr_tile_tsmqr"):
         getattr(L, nm).restype = _I
+    L.tqr_dist_plan_create.argtypes = [ctypes.POINTER(_P), _I, _I, _I, _I, _I, _I]
+    L.tqr_dist_handle_bytes.argtypes = [_P]
+    L.tqr_dist_handle_bytes.restype = ctypes.c_size_t
+    L.tqr_dist_export.argtypes = [_P, ctypes.c_char_p, ctypes.c_size_t]
+    L.tqr_dist_import.argtypes = [_P, ctypes.c_char_p, ctypes.c_size_t]
+    L.tqr_dist_reset.argtypes = [_P, _P]
+    L.tqr_plan_status.argtypes = [_P, _P]
     L.tqr_dgeqrt_host.argtypes = [_P, _P, _I, _I, _I, _I]
     L.tqr_sgeqrt_host.argtypes = [_P, _P, _I, _I, _I, _I]
     _lib = L
@@ -166,6 +173,71 @@ class TiledQR:
             lib().tqr_plan_destroy(self.h)
         except Exception:
             pass
+
+
+class DistTiledQR(TiledQR):
+    """One rank's share of a multi-GPU factorisation (tile-column cyclic partition, one process
+    per GPU; include/tqr.h "multi-GPU"). Tile column j belongs to rank j % world. The handle
+    exchange and the per-factorisation barrier go over torch.distributed (`group`); the panel
+    data moves GPU to GPU inside the persistent launch (xGMI stores into IPC-opened peer
+    workspaces), not through the collective library."""
+
+    def __init__(self, m, n, b, dtype, group=None):
+        import torch.distributed as dist
+        self.m, self.n, self.b = m, n, b
+        self.dtype = dtype if isinstance(dtype, int) else _dtype_code(dtype)
+        self.kmax = min(m, n) // b
+        self.group = group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        verbose = os.environ.get("TQR_DIST_VERBOSE") == "1"
+
+        def say(msg):
+            if verbose:
+                import sys
+                print(f"[rank {self.rank}] DistTiledQR: {msg}", file=sys.stderr, flush=True)
+
+        say("create")
+        h = _P()
+        check(lib().tqr_dist_plan_create(ctypes.byref(h), m, n, b, self.dtype, self.rank, self.world),
+              "tqr_dist_plan_create")
+        self.h = h
+        if self.world > 1:
+            say("export")
+            hb = lib().tqr_dist_handle_bytes(self.h)
+            buf = ctypes.create_string_buffer(hb)
+            check(lib().tqr_dist_export(self.h, buf, hb), "tqr_dist_export")
+            blocks = [None] * self.world
+            say("all_gather")
+            dist.all_gather_object(blocks, bytes(buf.raw), group=group)
+            allb = b"".join(blocks)
+            say("import")
+            check(lib().tqr_dist_import(self.h, allb, len(allb)), "tqr_dist_import")
+            say("ready")
+
+    def owns(self, tile_col):
+        return tile_col % self.world == self.rank
+
+    def execute(self, A, tau, ldda=None, stream=None):
+        """Reset this rank's counters, barrier over all ranks, launch (stream-ordered)."""
+        import torch
+        import torch.distributed as dist
+        ldda = ldda or self.m
+        if self.world > 1:
+            check(lib().tqr_dist_reset(self.h, _P(stream or 0)), "tqr_dist_reset")
+            torch.cuda.synchronize()
+            dist.barrier(group=self.group)
+        check(lib().tqr_plan_execute(self.h, _ptr(A), ldda, _ptr(tau), _P(stream or 0)), "tqr_plan_execute")
+
+    def status(self, stream=None):
+        check(lib().tqr_plan_status(self.h, _P(stream or 0)), "tqr_plan_status")
+
+
+def dist_plan_check(M, N, b, rank, world, seglen=8):
+    """Host-only: (ntasks, n_forward_tasks) of one rank's task list."""
+    nt, nf = _I(), _I()
+    check(lib().tqr_dist_plan_check(M, N, b, seglen, rank, world, ctypes.byref(nt), ctypes.byref(nf)),
+          "tqr_dist_plan_check")
+    return nt.value, nf.value
 
 
 def fill_randzo(A, m, n, seed, ldda=None, stream=None):

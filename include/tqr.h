@@ -72,6 +72,26 @@ int tqr_plan_stats(const tqr_plan* plan, int* nlaunch_update, double* ms_update,
 /* Number of flat-tree tasks (reference calcTotalTasks, src/gpucalc.cu:1546, for all m,n). */
 long tqr_total_tasks(int m, int n, int b);
 
+/* ---- multi-GPU: tile-column cyclic partition, one process per GPU ------------------------
+ * Rank r owns tile columns j with j % world == r and factors them in a full-size matrix of
+ * its own (only its columns are valid at the end; tau column k lives on rank k % world). The
+ * owner of panel k forwards each finished reflector group's V/T images to every peer over
+ * xGMI inside the persistent launch (peer workspaces opened by IPC), so panels of successive
+ * steps overlap across GPUs exactly as on one GPU. Sequence per factorisation, every rank:
+ *   tqr_dist_reset(plan, s); sync; <barrier over ranks>; tqr_plan_execute(plan, ...);
+ * Setup once: tqr_dist_export -> exchange all ranks' handle blocks (e.g. an all-gather over
+ * torch.distributed / MPI) -> tqr_dist_import(plan, blocks of rank 0..world-1). */
+int tqr_dist_plan_create(tqr_plan** plan, int m, int n, int b, int dtype, int rank, int world);
+/* bytes of one rank's handle block (IPC handles of its panel counters and per-step panel
+ * workspaces — one allocation per step keeps every export under 2 GiB) */
+size_t tqr_dist_handle_bytes(const tqr_plan* plan);
+int tqr_dist_export(tqr_plan* plan, void* handles, size_t len);
+int tqr_dist_import(tqr_plan* plan, const void* all_handles, size_t len);
+int tqr_dist_reset(tqr_plan* plan, void* stream);
+int tqr_dist_owner(const tqr_plan* plan, int tile_col);
+/* host-only: this rank's task-list length and number of forward tasks */
+int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd);
+
 /* ---- one-shot helpers ------------------------------------------------------------------ */
 /* Device pointers, stream-ordered; plan cached per (m,n,b,dtype). */
 int tqr_dgeqrt_tiled(int m, int n, int b, double* dA, int ldda, double* dtau_compact, void* stream);

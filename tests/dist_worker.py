@@ -1,0 +1,88 @@
+"""Multi-GPU parity worker (launched by tests/test_dist.py under torch.distributed.run).
+
+Every rank factorises the same RANDZO matrix with the tile-column partitioned engine
+(tqr.DistTiledQR); rank 0 also factorises it alone (tqr.TiledQR, the single-GPU engine). The
+owned tile columns and taus of all ranks are gathered to rank 0 (gloo, host tensors) and
+compared with the single-GPU result: the per-tile operation sequence is identical, so the
+results must agree bit for bit. Runs the factorisation twice (counter reset / re-launch path).
+Prints one JSON line on rank 0. Usage: dist_worker.py m n b f64|f32 [device]
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "gpu-tiled-qr-decomposition_amd"))
+import tqr  # noqa: E402
+
+
+def main():
+    m, n, b = (int(x) for x in sys.argv[1:4])
+    dt = torch.float64 if sys.argv[4] == "f64" else torch.float32
+    dev = int(sys.argv[5]) if len(sys.argv) > 5 else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    q, kmax = n // b, min(m, n) // b
+    A0 = torch.empty((n, m), dtype=dt, device="cuda")
+    tqr.fill_randzo(A0, m, n, 5)
+    torch.cuda.synchronize()
+    if os.environ.get("TQR_DIST_VERBOSE") == "1":
+        print(f"[rank {rank}] input ready", file=sys.stderr, flush=True)
+    plan = tqr.DistTiledQR(m, n, b, dt)
+    out = {}
+    verbose = os.environ.get("TQR_DIST_VERBOSE") == "1"
+
+    def say(msg):
+        if verbose:
+            print(f"[rank {rank}] {msg}", file=sys.stderr, flush=True)
+
+    for rep in range(2):
+        A = A0.clone()
+        tau = torch.zeros((kmax, m), dtype=dt, device="cuda")
+        say(f"run {rep}: execute")
+        plan.execute(A, tau)
+        say(f"run {rep}: launched")
+        plan.status()
+        say(f"run {rep}: done")
+        own = [j for j in range(q) if plan.owns(j)]
+        mine = {j: A[j * b:(j + 1) * b].cpu().numpy() for j in own}
+        mine_tau = {k: tau[k].cpu().numpy() for k in range(kmax) if plan.owns(k)}
+        allcols = [None] * world
+        dist.all_gather_object(allcols, (mine, mine_tau))
+        say(f"run {rep}: gathered")
+        if rank == 0:
+            ref = tqr.TiledQR(m, n, b, dt)
+            R = A0.clone()
+            rtau = torch.zeros((kmax, m), dtype=dt, device="cuda")
+            ref.execute(R, rtau)
+            torch.cuda.synchronize()
+            R = R.cpu().numpy()
+            rtau = rtau.cpu().numpy()
+            F = np.zeros_like(R)
+            T = np.zeros_like(rtau)
+            seen = set()
+            for cols, taus in allcols:
+                for j, blk in cols.items():
+                    F[j * b:(j + 1) * b] = blk
+                    seen.add(j)
+                for k, t in taus.items():
+                    T[k] = t
+            out[f"run{rep}"] = {
+                "cols_covered": len(seen) == q,
+                "max_diff": float(np.abs(F - R).max()),
+                "max_tau_diff": float(np.abs(T - rtau).max()),
+                "exact": bool(np.array_equal(F, R) and np.array_equal(T, rtau)),
+            }
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"m": m, "n": n, "b": b, "world": world, **out}))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Multi-rank engine probe on ONE GPU: 2 ranks (torch.distributed.run, gloo), each with a share of
+# the CUs (TQR_FLOW_GRID), tests/dist_worker.py at growing sizes; stops at the first failure.
+set -o pipefail
+mkdir -p gpurun_out/dist
+for cfg in ${DIST_CFGS:-"4096 4096 256 96" "16384 4096 256 96" "32768 8192 256 96" "32768 8192 256 128"}; do
+  set -- $cfg
+  echo "== m=$1 n=$2 b=$3 grid=$4" | tee -a gpurun_out/dist/probe.log
+  TQR_FLOW_GRID=$4 timeout -k 10 100 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29512 tests/dist_worker.py $1 $2 $3 f64 0 >> gpurun_out/dist/probe.log 2>&1
+  rc=$?
+  echo "rc $rc" | tee -a gpurun_out/dist/probe.log
+  [ $rc = 0 ] || break
+done

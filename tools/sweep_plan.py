@@ -4,7 +4,7 @@ m = sys.argv[1] if len(sys.argv) > 1 else "16384"
 for seg in ["8", "4", "16"]:
     for tg in ["0.7", "1.0", "1.4", "2.0"]:
         env = dict(os.environ, TQR_TG=tg, TQR_SEGLEN=seg)
-        r = subprocess.run([sys.executable, "bench.py", "--no-cpu-baseline", "--steps", "3", "--warmup", "1", "--m", m, "--n", m],
+        r = subprocess.run([sys.executable, "bench.py", "--no-cpu-baseline", "--steps", "3", "--warmup", "1", "--rows", m, "--cols", m],
                            env=env, capture_output=True, text=True, timeout=120)
         try:
             j = json.loads(r.stdout.strip().splitlines()[-1])

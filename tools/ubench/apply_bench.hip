@@ -5,6 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include "tiles.hpp"
+#include "gridscheduler.h"
+namespace tqr { struct Item { int ts, l, m, k; }; }
+#include "flow.hpp"
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 using namespace tqr;
 constexpr int B = 256;
@@ -195,6 +198,36 @@ __global__ __launch_bounds__(256, 1) void k_apply2(double* out, int iters) {
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+
+// the chain's group step without global data dependencies: apply_zw with the next group's
+// LDS-DMA in its hook (DMA on/off), apply_x, vmcnt(0) + barrier per group
+template <bool DMA>
+__global__ __launch_bounds__(256, 1) void k_apply_dma(double* out, const double* img, int iters) {
+  extern __shared__ __align__(16) double lds[];
+  constexpr int BUF = G::VIMG + G::TIMG;
+  for (int i = threadIdx.x; i < 2 * BUF; i += 256) lds[i] = 1e-3 * ((i * 37) % 101 - 50) / 50.0;
+  __syncthreads();
+  double X[G::NKS], H[G::NRI], W[G::NRI];
+  for (int k = 0; k < G::NKS; ++k) X[k] = 1.0 + 1e-3 * (threadIdx.x + k);
+  for (int r = 0; r < G::NRI; ++r) H[r] = 0.5 + 1e-3 * r;
+  int buf = 0;
+  for (int it = 0; it < iters; ++it) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const double* Vs = lds + buf * BUF;
+    const double* src = img + (size_t)((it + blockIdx.x) % 512) * BUF;
+    DmaJob<B> d{lds + (buf ^ 1) * BUF, src, src + G::VIMG, DMA};
+    apply_zw<B, true>(Vs, Vs + G::VIMG, X, H, W, 0, d);
+    apply_x<B, true>(Vs, X, W, 0);
+    buf ^= 1;
+  }
+  double s = 0;
+  for (int k = 0; k < G::NKS; ++k) s += X[k];
+  for (int r = 0; r < G::NRI; ++r) s += H[r];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 int main() {
   hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
   const int blocks = p.multiProcessorCount, iters = 2000;
@@ -206,6 +239,19 @@ int main() {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   k_apply<<<blocks, 256, lds>>>(out, iters / 4);
   CK(hipDeviceSynchronize());
+  {
+    double* img; CK(hipMalloc(&img, sizeof(double) * 9856 * 520)); CK(hipMemset(img, 0, sizeof(double) * 9856 * 520));
+    const size_t l2 = 2 * (G::VIMG + G::TIMG) * 8;
+    CK(hipFuncSetAttribute((const void*)k_apply_dma<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2));
+    CK(hipFuncSetAttribute((const void*)k_apply_dma<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l2));
+    for (int rep = 0; rep < 4; ++rep) {
+      float ms;
+      CK(hipEventRecord(e0));
+      if (rep & 1) k_apply_dma<true><<<blocks, 256, l2>>>(out, img, iters); else k_apply_dma<false><<<blocks, 256, l2>>>(out, img, iters);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("group step %s: %.2f us/group\n", (rep & 1) ? "with DMA   " : "without DMA", ms * 1e3 / iters);
+    }
+  }
   for (int rep = 0; rep < 3; ++rep) {
     float ms;
     CK(hipEventRecord(e0)); k_apply2<<<blocks, 256, lds>>>(out, iters / 2); CK(hipEventRecord(e1));
