@@ -59,7 +59,7 @@ __device__ unsigned long long g_pstamps[8];
 #endif
 
 #ifdef TQR_FLOW_STAMPS
-__device__ unsigned long long g_fst[4096 * 8];
+__device__ unsigned long long g_fst[4096 * 12];
 #endif
 }  // namespace tqr
 #include "flow.hpp"
@@ -334,7 +334,7 @@ struct FlowPlan {
 };
 
 static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
-  const int kmax = std::min(p, q), ns = (b + 63) / 64, ng = b / (b < 32 ? b : 32);
+  const int kmax = std::min(p, q), ns = (b + FLOW_SW - 1) / FLOW_SW, ng = b / (b < 32 ? b : 32);
   // cost model (unit: one chain element): Tg = one panel group-step; tunable for experiments
   const char* eg = getenv("TQR_TG");
   const double Tg = eg ? atof(eg) : 1.4, Te = 1.0;
@@ -542,7 +542,7 @@ struct tqr_plan {
   int engine = 1;          // 1 = persistent dataflow (default), 0 = wave-batched launches
   Item* d_flow = nullptr;
   int nflow = 0;
-  int* d_sync = nullptr;   // next, err, Rc, Tc, Ac
+  int* d_sync = nullptr;   // next, err, Rc, Tc, Ac, Rt
   size_t sync_ints = 0;
   int ns = 1, ng = 1, grid = 256, est_order = 0;
   ffn kflow = nullptr;
@@ -701,7 +701,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
   pl->ldsP = lds_panel(b);
   pl->ldsU = lds_update(b);
   // persistent dataflow engine: task list, progress counters, panel workspaces, kernel
-  pl->ns = (b + 63) / 64;
+  pl->ns = (b + FLOW_SW - 1) / FLOW_SW;  // chain strips per tile
   pl->ng = b / ib;
   {
     FlowPlan fp;
@@ -710,7 +710,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
-    pl->sync_ints = 2 + (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns + (size_t)pl->kmax * pl->q * pl->ns;
+    pl->sync_ints = 2 + 2 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns + (size_t)pl->kmax * pl->q * pl->ns;
     if (pl->nflow <= 0 || hipMalloc(&pl->d_flow, sizeof(Item) * pl->nflow) != hipSuccess ||
         hipMalloc(&pl->d_sync, sizeof(int) * pl->sync_ints) != hipSuccess ||
         hipMalloc(&pl->d_wk, sizeof(double*) * pl->kmax) != hipSuccess) {
@@ -885,6 +885,7 @@ int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream)
     f.next = pl->d_sync; f.err = pl->d_sync + 1; f.Rc = pl->d_sync + 2;
     f.Tc = f.Rc + (size_t)pl->kmax * pl->ng;
     f.Ac = f.Tc + (size_t)pl->p * pl->q * pl->ns;
+    f.Rt = f.Ac + (size_t)pl->kmax * pl->q * pl->ns;
     f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.peers = pl->d_peers; f.Fc = pl->d_fc;
     if (pl->world > 1) f.Rc = pl->d_rc;  // counters reset by tqr_dist_reset (all ranks, then a barrier)
     else HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
@@ -1170,10 +1171,10 @@ extern "C" int tqr_debug_stamps(unsigned long long* out, int reset) {
 #endif
 
 #ifdef TQR_FLOW_STAMPS
-// per-workgroup activity sums of the last k_flow launch (8 categories, flow.hpp FST)
+// per-workgroup activity sums of the last k_flow launch (FST_N categories, flow.hpp FST)
 extern "C" int tqr_debug_flow_stamps(unsigned long long* out, int nblocks) {
   if (nblocks > 4096) return TQR_EINVAL;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fst), sizeof(unsigned long long) * 8 * nblocks) != hipSuccess) return TQR_EHIP;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fst), sizeof(unsigned long long) * FST_N * nblocks) != hipSuccess) return TQR_EHIP;
   return TQR_OK;
 }
 #endif

@@ -10,6 +10,11 @@
 //                   UNMQR(k,j) (segment 0 only), TSMQR(i,j,k) for i in [i0,i1). The strip of
 //                   tile (k,j) (the TSMQR head rows) stays owned by the chain across elements.
 // Progress counters (zeroed per factorisation):
+//   Rt[k][g]   members of panel k that finished the in-tile trailing update of group g (the R_kk
+//              head rows of the group's columns right of it): the next member's trailing update
+//              waits for it, its factorisation of group g does not (it needs only the 32 x 32
+//              diagonal block, final at Rc) — so members are spaced by max(factor, trailing)
+//              instead of their sum;
 //   Rc[k][g]   members of panel k (GEQRT(k), TSQRT(k+1,k), ...) that finished group g — a
 //              TSQRT's group g may start once its predecessor finished group g, so the flat
 //              TS chain is pipelined at group (32-reflector) granularity, not tile granularity;
@@ -30,7 +35,9 @@ constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel memb
 // Every FST(c) charges the time since the previous stamp to category c (LDS-resident sums,
 // thread 0 only, written to g_fst[blockIdx.x][*] at exit). Categories: 0 chain waits,
 // 1 panel waits, 2 chain head-row I/O, 3 chain apply (with the LDS-DMA issue), 4 chain strip
-// I/O + publish, 5 panel compute, 6 dequeue/dispatch + kernel exit, 7 chain drain + barrier.
+// I/O + publish, 5 panel compute, 6 dequeue/dispatch + kernel exit, 7 chain drain + barrier,
+// 8 chain Tc waits (tile's previous step), 9 chain Ac waits (previous segment).
+constexpr int FST_N = 12;
 #ifdef TQR_FLOW_STAMPS
 extern __device__ unsigned long long g_fst[];
 #define FST(c)                                                                            \
@@ -45,7 +52,15 @@ extern __device__ unsigned long long g_fst[];
 #else
 #define FST(c) do {} while (0)
 #endif
+// 256 threads = 4 waves = one wave per SIMD (the register budget of the chain: X strip 128 VGPRs,
+// operands and prefetches in the accumulator file). An 8-wave / 128-column-strip variant
+// (FLOW_NT = 512: half the LDS-DMA bytes per flop, two waves per SIMD, apply_zw/apply_x without
+// read pipelining — 64.8 TF/s in tools/ubench/apply_bench.hip) compiles, but the chain then
+// exceeds the 256-register budget of two waves per SIMD and spills inside the MFMA loops.
 constexpr int FLOW_NT = 256;
+constexpr int FLOW_NW = FLOW_NT / 64;      // waves
+constexpr int FLOW_SW = 16 * FLOW_NW;      // strip width (columns) of a chain task
+constexpr bool FLOW_PF = FLOW_NW <= 4;     // software-pipelined operand reads (1 wave/SIMD)
 constexpr unsigned long long FLOW_TIMEOUT = 500000000ull;  // 5 s of s_memrealtime (100 MHz)
 
 // Multi-GPU (tile-column cyclic partition, one process per GPU): peer buffers opened by IPC.
@@ -69,6 +84,7 @@ struct FlowArgs {
   int* Rc;
   int* Tc;
   int* Ac;
+  int* Rt;
   // multi-GPU: dist = world > 1. Rc then lives in uncached memory written by peers' forward
   // tasks over xGMI and is accessed at system scope; Fc[k][g] orders this rank's forwards.
   int dist, rank, world;
@@ -157,7 +173,7 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 template <int B>
 struct DmaJob {
   static constexpr int NIV = Geo<B>::VIMG / 128, NIT = Geo<B>::TIMG / 128;
-  static constexpr int PV = (NIV + 3) / 4, PT = (NIT + 3) / 4;
+  static constexpr int PV = (NIV + FLOW_NW - 1) / FLOW_NW, PT = (NIT + FLOW_NW - 1) / FLOW_NW;
   static constexpr int STEPS = PV + PT;
   double* dst;
   const double* v;
@@ -165,13 +181,14 @@ struct DmaJob {
   bool on;
   __device__ __forceinline__ void step(int m) const {
     if (!on) return;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // wave id made provably uniform: addresses = scalar base + one per-lane offset register
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (m < PV) {
-      const int u = w + 4 * m;
+      const int u = w + FLOW_NW * m;
       if (u < NIV)
         __builtin_amdgcn_global_load_lds((glb_void_t*)(v + u * 128 + 2 * lane), (lds_void_t*)(dst + u * 128), 16, 0, 16);
     } else if (m < STEPS) {
-      const int u = w + 4 * (m - PV);
+      const int u = w + FLOW_NW * (m - PV);
       if (u < NIT)
         __builtin_amdgcn_global_load_lds((glb_void_t*)(t + u * 128 + 2 * lane),
                                          (lds_void_t*)(dst + Geo<B>::VIMG + u * 128), 16, 0, 16);
@@ -185,7 +202,7 @@ struct DmaJob {
 // from a parity-alternating LDS slot (a slot is rewritten only after the next barrier).
 template <bool DRAIN>
 __device__ __forceinline__ bool sync_point(bool ok0, int* sflag, int& par) {
-  int* slot = sflag + 24 + par;  // LDS tail: [task][flag][FST sums 2..19][..][verdicts 25,26][..][Rc view 33..]
+  int* slot = sflag + 40 + par;  // LDS tail: [task][flag][FST sums 2..25][..][verdicts 41,42][..][Rc view 49..]
   par ^= 1;
   if (threadIdx.x == 0) *slot = ok0 ? 1 : 0;
   if (DRAIN) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -205,16 +222,32 @@ __device__ __forceinline__ void publish_after_drain(int* p, int delta) {
 // the images are write-once inside a launch (one producer, stored sc1 and drained before its
 // counter add), no workgroup reads a slot before observing its counter, and the DMA itself is
 // an sc1 (L1-bypassing) load — so no CU can hold a stale copy of an image line.
+// prefetch() (thread 0, right after a sync point) issues the row's loads early, so that the next
+// ensure() normally finds fresh values without an exposed round trip.
 template <int NG>
 struct PanelView {
   int* rv;
+  int pf[NG];
+  bool pf_valid;
   __device__ __forceinline__ void init(int* lds_words) {
     rv = lds_words;
+    pf_valid = false;
     if (threadIdx.x == 0)
       for (int g = 0; g < NG; ++g) rv[g] = 0;
   }
+  __device__ __forceinline__ void prefetch(int* rc, bool sys) {
+#pragma unroll
+    for (int x = 0; x < NG; ++x) pf[x] = ld_cnt(rc + x, sys);
+    pf_valid = true;
+  }
   __device__ __forceinline__ bool ensure(int* rc, int g, int need, int* err, bool sys) {
     if (rv[g] >= need) return true;
+    if (pf_valid) {
+#pragma unroll
+      for (int x = 0; x < NG; ++x) rv[x] = max(rv[x], pf[x]);
+      pf_valid = false;
+      if (rv[g] >= need) return true;
+    }
     int v[NG];
 #pragma unroll
     for (int x = 0; x < NG; ++x) v[x] = ld_cnt(rc + x, sys);
@@ -318,23 +351,31 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       for (int idx = t; idx < G::TSZ; idx += FLOW_NT) st(tg + idx, Ts[idx]);
       for (int idx = t; idx < G::VSZ; idx += FLOW_NT) st(vg + idx, Vs[vimg_row(idx / VP) * VP + idx % VP]);
     }
+    // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
+    wg_publish(&a.Rc[(size_t)k * NG + g], 1, a.dist);
+    if (!qrs) {  // R_kk head rows right of the group as left by the previous member's trailing
+      FST(5);
+      const bool ok = t == 0 ? spin_ge(&a.Rt[(size_t)k * NG + g], pos, a.err) : true;
+      if (!wg_verdict(ok, sflag)) return;
+      FST(1);
+    }
     const int nstr = (B - c0 - IB) / 16;
     for (int s = w; s < nstr; s += FLOW_NT / 64) {
       asm volatile("" ::: "memory");
       const int col = c0 + IB + 16 * s;
       if (qrs) {
         load_strip<B, S, true>(X, Rt, ldm, col, ks0);
-        apply_group<B, false>(Vs, Ts, X, H, ks0);
+        apply_group<B, false, FLOW_PF>(Vs, Ts, X, H, ks0);
         store_strip<B>(X, Rt, ldm, col, ks0);
       } else {
         load_strip<B, S, true>(X, Bt, ldm, col, 0);
         load_head<B, S, true>(H, Rt, ldm, c0, col);
-        apply_group<B, true>(Vs, Ts, X, H, 0);
+        apply_group<B, true, FLOW_PF>(Vs, Ts, X, H, 0);
         store_strip<B>(X, Bt, ldm, col, 0);
         store_head<B>(H, Rt, ldm, c0, col);
       }
     }
-    wg_publish(&a.Rc[(size_t)k * NG + g], 1, a.dist);
+    wg_publish(&a.Rt[(size_t)k * NG + g], 1);
   }
   FST(5);
 }
@@ -397,7 +438,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
   S* A = (S*)a.A;
   const size_t ldm = a.ldm;
   const int t = threadIdx.x, w = t >> 6;
-  const int col = s * 64 + 16 * w;  // this wave's 16 columns inside the tile
+  const int col = s * FLOW_SW + 16 * w;  // this wave's 16 columns inside the tile
   const bool active = col < B;
   S* At = A + (size_t)j * B * ldm + (size_t)k * B;  // tile (k,j): the chain's head rows
   int* const rc = &a.Rc[(size_t)k * NG];
@@ -409,7 +450,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
   int* pending = nullptr;
   bool dma_next = false;  // group 0 of the next element already in flight
   PanelView<NG> pv;
-  pv.init(sflag + 32);
+  pv.init(sflag + 48);
+  int tc_pf = -1;  // thread 0: Tc of the next element's tile, loaded one group ahead
   FST(6);
   const int ifirst = seg == 0 ? k : i0;
   for (int i = ifirst; i < i1 || i == k; i = (i == k ? i0 : i + 1)) {
@@ -419,7 +461,10 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
       bool ok = true;
       if (t == 0) {
         if (i == ifirst && seg > 0) ok = spin_ge(ac, seg, a.err);
-        if (ok && k > 0) ok = spin_ge(tc(i), k, a.err);
+        FST(9);
+        if (ok && k > 0 && tc_pf < k) ok = spin_ge(tc(i), k, a.err);
+        tc_pf = -1;
+        FST(8);
         if (ok && !dma_next) ok = pv.ensure(rc, 0, need, a.err, a.dist);
       }
       FST(0);
@@ -434,8 +479,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
     }
     dma_next = false;
     // head rows: written by another workgroup before this segment (sc1 loads) or by this one
-    if (ts && active) {
-      if (i == ifirst || i == k + 1) load_head<B, S, true>(H, At, ldm, 0, col);
+    const bool first_ts = i == ifirst || i == k + 1;  // head rows last written by another workgroup
+    if (FLOW_PF && ts && active) {
+      if (first_ts) load_head<B, S, true>(H, At, ldm, 0, col);
       else load_head<B, S, false>(H, At, ldm, 0, col);
     }
     FST(4);
@@ -455,7 +501,15 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
         publish_after_drain(pending, 1);
         pending = nullptr;
       }
+      if (t == 0) {  // early loads of the counters the next sync point will test
+        pv.prefetch(rc, a.dist);
+        if (g + 1 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
+      }
       FST(7);
+      if (!FLOW_PF && ts && active) {  // two waves per SIMD: load the group's head rows here
+        if (first_ts) load_head<B, S, true>(H, At, ldm, g * IB, col);
+        else load_head<B, S, false>(H, At, ldm, g * IB, col);
+      }
       const double* Vs = lds + buf * BUF;
       const double* Ts = Vs + G::VIMG;
       // the other buffer is free (every wave passed this sync point): next DMA rides phase 1
@@ -471,8 +525,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
         dma_next = true;
       }
       if (active) {
-        if (ts) apply_zw<B, true>(Vs, Ts, X, H, W, 0, d);
-        else apply_zw<B, false>(Vs, Ts, X, H, W, g * IB / 4, d);
+        if (ts) apply_zw<B, true, DmaJob<B>, FLOW_PF>(Vs, Ts, X, H, W, 0, d);
+        else apply_zw<B, false, DmaJob<B>, FLOW_PF>(Vs, Ts, X, H, W, g * IB / 4, d);
       } else {
         for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
       }
@@ -481,19 +535,21 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
         // head rows stay with this workgroup for the whole segment: plain (write-back) stores,
         // made visible to the next segment's workgroup by one release before the Ac publish
         store_head_plain<B>(H, At, ldm, g * IB, col);
-        if (g + 1 < NG) {
-          if (i == ifirst || i == k + 1) load_head<B, S, true>(Hn, At, ldm, (g + 1) * IB, col);
+        if (FLOW_PF && g + 1 < NG) {
+          if (first_ts) load_head<B, S, true>(Hn, At, ldm, (g + 1) * IB, col);
           else load_head<B, S, false>(Hn, At, ldm, (g + 1) * IB, col);
         }
       }
       FST(2);
       if (active) {
-        if (ts) apply_x<B, true>(Vs, X, W, 0);
-        else apply_x<B, false>(Vs, X, W, g * IB / 4);
+        if (ts) apply_x<B, true, FLOW_PF>(Vs, X, W, 0);
+        else apply_x<B, false, FLOW_PF>(Vs, X, W, g * IB / 4);
       }
       FST(3);
+      if (FLOW_PF) {
 #pragma unroll
-      for (int r = 0; r < G::NRI; ++r) H[r] = Hn[r];
+        for (int r = 0; r < G::NRI; ++r) H[r] = Hn[r];
+      }
       buf ^= 1;
     }
     if (active) store_strip_pair<B, S>(X, Xt, ldm, col);
@@ -526,7 +582,7 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
   if (threadIdx.x == 0) {
     unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 2);
     l_[0] = __builtin_amdgcn_s_memrealtime();
-    for (int c = 0; c < 8; ++c) l_[1 + c] = 0;
+    for (int c = 0; c < FST_N; ++c) l_[1 + c] = 0;
   }
   int* sflag = s_flag;
 #endif
@@ -556,7 +612,7 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
   FST(6);
   if (threadIdx.x == 0) {
     unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 2);
-    for (int c = 0; c < 8; ++c) g_fst[blockIdx.x * 8 + c] = l_[1 + c];
+    for (int c = 0; c < FST_N; ++c) g_fst[blockIdx.x * FST_N + c] = l_[1 + c];
   }
 #endif
 }

@@ -86,20 +86,15 @@ void testDAPP(float* timings, int n, int nblocks) {
   (void)hipFree(dT);
 }
 
-// One TSMQR on a 64 x 64 fp32 matrix (gpucalc.cu:1776-1799): V = tile (1,0), tau = its
-// diagonal entries as stored by the reference (tau of tile (1,0) at rows 32.., column 0 of a
-// tau matrix is not passed in the reference either; it uses mat's own layout), A = (0,1),
-// B = (1,1). Here tau is taken as 2/(1+|v|^2) of each V column, i.e. V is treated as a
-// TSQRT output.
+// One TSMQR on a 64 x 64 fp32 matrix, as the reference's doCUDADAPP (gpucalc.cu:1776-1799):
+// V = tile (1,0), A = tile (0,1), B = tile (1,1), and — exactly as the reference passes
+// `dev_mat` as the Tau argument — the 32 taus are the first 32 entries of the matrix (column 0
+// of tile (0,0)), which the update does not touch.
 void doCUDADAPP(float* mat) {
   if (!mat) return;
   const int b = 32, ldm = 64;
   float tau[32];
-  for (int c = 0; c < b; ++c) {
-    double s = 1.0;
-    for (int r = 0; r < b; ++r) s += (double)mat[(size_t)c * ldm + b + r] * mat[(size_t)c * ldm + b + r];
-    tau[c] = (float)(2.0 / s);
-  }
+  for (int c = 0; c < b; ++c) tau[c] = mat[c];
   int st = tqr_tile_tsmqr(TQR_F32, mat + b, mat + (size_t)b * ldm, mat + (size_t)b * ldm + b, tau, b, ldm);
   if (st) die("doCUDADAPP", st);
 }

@@ -114,7 +114,9 @@ struct NoHook {
   __device__ __forceinline__ void step(int) const {}
   static constexpr int STEPS = 0;
 };
-template <int B, bool HEAD, typename Hook = NoHook>
+// PF: software-pipelined LDS operand reads (needed at one wave per SIMD; at two waves per SIMD
+// the other wave hides the latency and the registers are better spent elsewhere)
+template <int B, bool HEAD, typename Hook = NoHook, bool PF = true>
 __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const double* __restrict__ Ts,
                                          const double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI],
                                          double (&W)[Geo<B>::NRI], int ks0, const Hook& hook = Hook()) {
@@ -137,17 +139,20 @@ __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const do
     }
   };
   double ac[NRI], an[NRI];
-  ldz(ac, HEAD ? 0 : ks0);
+  if (PF) ldz(ac, HEAD ? 0 : ks0);
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
     asm volatile("" ::: "memory");  // one k-step per region: bounds the hoisting of LDS reads
     if ((ks & 1) == 0) hook.step(ks / 2);
     if (!HEAD && ks < ks0) continue;
-    if (ks + 1 < NKS) ldz(an, ks + 1);
+    if (!PF) ldz(ac, ks);
+    else if (ks + 1 < NKS) ldz(an, ks + 1);
 #pragma unroll
     for (int r = 0; r < NRI; ++r) Z[r] = mfma4(ac[r], X[ks], Z[r]);
+    if (PF) {
 #pragma unroll
-    for (int r = 0; r < NRI; ++r) ac[r] = an[r];
+      for (int r = 0; r < NRI; ++r) ac[r] = an[r];
+    }
   }
   for (int m = NKS / 2; m < Hook::STEPS; ++m) hook.step(m);
   // W = -T^T Z   (A operand: T[4k2+x][4wi+y]); T upper triangular -> k2 <= wi.
@@ -164,7 +169,7 @@ __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const do
   }
 }
 
-template <int B, bool HEAD>
+template <int B, bool HEAD, bool PF = true>
 __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&X)[Geo<B>::NKS],
                                         const double (&W)[Geo<B>::NRI], int ks0) {
   using g = Geo<B>;
@@ -182,13 +187,18 @@ __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&
   };
   double bc[2][NRI], bn[2][NRI];
   const int kx = HEAD ? 0 : (ks0 & ~1);
-  ldx(bc[0], kx);
-  ldx(bc[1], kx + 1);
+  if (PF) {
+    ldx(bc[0], kx);
+    ldx(bc[1], kx + 1);
+  }
 #pragma unroll
   for (int kb = 0; kb < NKS; kb += 2) {
     asm volatile("" ::: "memory");
     if (!HEAD && kb + 1 < ks0) continue;
-    if (kb + 2 < NKS) {
+    if (!PF) {
+      ldx(bc[0], kb);
+      ldx(bc[1], kb + 1);
+    } else if (kb + 2 < NKS) {
       ldx(bn[0], kb + 2);
       ldx(bn[1], kb + 3);
     }
@@ -197,19 +207,21 @@ __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&
 #pragma unroll
       for (int u = 0; u < 2; ++u)
         if (HEAD || kb + u >= ks0) X[kb + u] = mfma4(bc[u][wi], W[wi], X[kb + u]);
+    if (PF) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int r = 0; r < NRI; ++r) bc[u][r] = bn[u][r];
+        for (int r = 0; r < NRI; ++r) bc[u][r] = bn[u][r];
+    }
   }
 }
 
-template <int B, bool HEAD>
+template <int B, bool HEAD, bool PF = true>
 __device__ __forceinline__ void apply_group(const double* __restrict__ Vs, const double* __restrict__ Ts,
                                             double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI], int ks0) {
   double W[Geo<B>::NRI];
-  apply_zw<B, HEAD>(Vs, Ts, X, H, W, ks0);
-  apply_x<B, HEAD>(Vs, X, W, ks0);
+  apply_zw<B, HEAD, NoHook, PF>(Vs, Ts, X, H, W, ks0);
+  apply_x<B, HEAD, PF>(Vs, X, W, ks0);
 }
 
 // Strip loads/stores: X[ks] <- tile(rows 4ks+x, column col0 + 4blk + y).
@@ -487,7 +499,7 @@ __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Hs, 
   const int cw = J0 + rs_col<NW>(lane);
   const bool wr = (lane & (SPAN - 1)) == 0;
   double* rb = red + (C & 1) * 128;
-  if (wr) rb[w * 32 + cw] = ws;
+  if (wr && w < 4) rb[w * 32 + cw] = ws;  // rows live in waves 0-3 (a 512-thread workgroup's 4-7 idle)
   if (!TS && t == rc) {
 #pragma unroll
     for (int j = C; j < IB; ++j) hrow[(C & 1) * 32 + j] = x[j];
@@ -505,8 +517,8 @@ __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Hs, 
   const double scale = norm != 0.0 ? rcp_nr(hd) : 1.0;
   const double tau = 2.0 * rcp_nr(fma(scale * scale, dc, 1.0));
   const double fm = tau * fma(scale, Dm, Hm);  // f_j for j = cw
-  double* fb = wb + w * 32;
-  if (wr) fb[cw] = fm;
+  double* fb = wb + (w & 3) * 32;
+  if (wr && w < 4) fb[cw] = fm;
   if (TS && w == 0 && wr && cw >= C) hout[C * TP + cw] = Hm - fm;  // cw == C: R_CC = x0 - f_C
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -565,7 +577,7 @@ __device__ void panel_factor(double* Vs, double* Hs, double* tauv, double* scrat
   }
   __syncthreads();
   if (TS) {
-    for (int idx = t; idx < IB * IB; idx += NT) {
+    for (int idx = t; idx < IB * IB; idx += blockDim.x) {
       const int r = idx / IB, c = idx % IB;
       if (r <= c) Hs[r * TP + c] = hout[r * TP + c];
     }
@@ -614,14 +626,15 @@ __device__ void build_t(const double* Vs, const double* tauv, double* Gs, double
         for (int r = 0; r < NRI; ++r) Z[h][r] = mfma4(a[r], xb, Z[h][r]);
       }
     }
-    double* gp = Gp + w * IB * TP;
+    double* gp = Gp + (w & 3) * IB * TP;
+    if (w < 4)
 #pragma unroll
     for (int h = 0; h < NCH; ++h)
 #pragma unroll
       for (int r = 0; r < NRI; ++r) gp[(4 * r + x) * TP + 16 * h + 4 * blk + y] = Z[h][r];
   }
   __syncthreads();
-  for (int idx = t; idx < IB * IB; idx += NT) {
+  for (int idx = t; idx < IB * IB; idx += blockDim.x) {
     const int r = idx / IB, c = idx % IB, o = r * TP + c;
     Gs[o] = (Gp[o] + Gp[IB * TP + o]) + (Gp[2 * IB * TP + o] + Gp[3 * IB * TP + o]);
   }

@@ -101,3 +101,22 @@ def test_tile_zero_and_unit_columns(tqr, oracle, b):
         Xo, to = oracle_tile(oracle, op, X0, b)
         Xg, tg = run_tile(tqr, op, X0, b)
         assert close(tg, to) and close(Xg, Xo), op
+
+
+def test_docudadapp_matches_oracle(tqr, oracle):
+    """doCUDADAPP (reference gpucalc.cu:1776): one TSMQR on a 64 x 64 fp32 matrix with
+    V = tile (1,0), A = tile (0,1), B = tile (1,1) and tau = the matrix's first 32 entries."""
+    import ctypes
+    b, ldm = 32, 64
+    M = oracle.randzo(64, 64, np.float32, seed=7)
+    M[0, :b] = np.linspace(0.5, 1.5, b, dtype=np.float32)  # plausible taus in column 0
+    ref = M.copy()
+    tau = ref[0, :b].copy()
+    P = ctypes.c_void_p
+    es = ref.itemsize
+    base = ref.ctypes.data
+    oracle.L.oracle_tsmqr_s(P(base + b * es), P(base + b * ldm * es), P(base + (b * ldm + b) * es),
+                            tau.ctypes.data_as(P), b, b, ldm)
+    G = M.copy()
+    tqr.lib().doCUDADAPP(G.ctypes.data_as(P))
+    assert float(np.abs(G.astype(np.float64) - ref.astype(np.float64)).max()) <= 1e-4 * max(1.0, float(np.abs(ref).max()))

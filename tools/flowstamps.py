@@ -20,12 +20,14 @@ for rep in range(2):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
 nb = torch.cuda.get_device_properties(0).multi_processor_count
-st = (ctypes.c_ulonglong * (8 * nb))()
+NC = 12
+st = (ctypes.c_ulonglong * (NC * nb))()
 assert L.tqr_debug_flow_stamps(st, nb) == 0
-names = ["chain polls (thread 0)", "panel waits", "chain head-row I/O", "chain apply (+DMA issue)",
-         "chain strip I/O+publish", "panel compute", "dequeue/dispatch/exit", "chain drain+barrier"]
-tot = [sum(st[w * 8 + c] for w in range(nb)) for c in range(8)]
+names = ["chain Rc polls (thread 0)", "panel waits", "chain head-row I/O", "chain apply (+DMA issue)",
+         "chain strip I/O+publish", "panel compute", "dequeue/dispatch/exit", "chain drain+barrier",
+         "chain Tc waits", "chain Ac waits", "-", "-"]
+tot = [sum(st[w * NC + c] for w in range(nb)) for c in range(NC)]
 allt = sum(tot)
 print(f"{m}x{n} b={b}: wall {ms:.1f} ms; {nb} workgroups; sum of stamps {allt / nb / 1e5:.1f} ms per WG")
-for c in range(8):
+for c in range(10):
     print(f"  {names[c]:24s} {tot[c] / nb / 1e5:8.2f} ms/WG  {100.0 * tot[c] / allt:5.1f}%")

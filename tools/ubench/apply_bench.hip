@@ -228,10 +228,31 @@ __global__ __launch_bounds__(256, 1) void k_apply_dma(double* out, const double*
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+
+// 8 waves per workgroup (two per SIMD), reads not software-pipelined
+__global__ __launch_bounds__(512, 1) void k_apply8(double* out, int iters) {
+  extern __shared__ __align__(16) double lds[];
+  double* Vs = lds;
+  double* Ts = Vs + G::VSZ;
+  for (int i = threadIdx.x; i < G::VSZ + G::TSZ; i += 512) lds[i] = 1e-3 * ((i * 37) % 101 - 50) / 50.0;
+  __syncthreads();
+  double X[G::NKS], H[G::NRI];
+  for (int k = 0; k < G::NKS; ++k) X[k] = 1.0 + 1e-3 * (threadIdx.x + k);
+  for (int r = 0; r < G::NRI; ++r) H[r] = 0.5 + 1e-3 * r;
+  for (int it = 0; it < iters; ++it) {
+    asm volatile("" ::: "memory");
+    apply_group<B, true, false>(Vs, Ts, X, H, 0);
+  }
+  double s = 0;
+  for (int k = 0; k < G::NKS; ++k) s += X[k];
+  for (int r = 0; r < G::NRI; ++r) s += H[r];
+  out[blockIdx.x * 512 + threadIdx.x] = s;
+}
+
 int main() {
   hipDeviceProp_t p; CK(hipGetDeviceProperties(&p, 0));
   const int blocks = p.multiProcessorCount, iters = 2000;
-  double* out; CK(hipMalloc(&out, blocks * 256 * sizeof(double)));
+  double* out; CK(hipMalloc(&out, blocks * 512 * sizeof(double)));
   const size_t lds = (G::VSZ + G::TSZ) * sizeof(double);
   CK(hipFuncSetAttribute((const void*)k_apply, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   CK(hipFuncSetAttribute((const void*)k_apply2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -239,6 +260,14 @@ int main() {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   k_apply<<<blocks, 256, lds>>>(out, iters / 4);
   CK(hipDeviceSynchronize());
+  CK(hipFuncSetAttribute((const void*)k_apply8, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  for (int rep = 0; rep < 3; ++rep) {
+    float ms;
+    CK(hipEventRecord(e0)); k_apply8<<<blocks, 512, lds>>>(out, iters); CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1)); CK(hipEventElapsedTime(&ms, e0, e1));
+    const double fl = (double)blocks * 8 * iters * 4.0 * B * G::IB * 16;
+    printf("8-wave WG, 2 waves/SIMD, no read pipelining: %.2f TFLOP/s (%.1f%% of 78.6), %.2f us per group (128 cols)\n", fl / ms / 1e9, fl / ms / 1e9 / 78.6 * 100, ms * 1e3 / iters);
+  }
   {
     double* img; CK(hipMalloc(&img, sizeof(double) * 9856 * 520)); CK(hipMemset(img, 0, sizeof(double) * 9856 * 520));
     const size_t l2 = 2 * (G::VIMG + G::TIMG) * 8;
