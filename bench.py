@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--rows", type=int, default=None, help="m (default 16384 at N=1, 65536 at N>1)")
     ap.add_argument("--cols", type=int, default=None, help="n (default 16384)")
     ap.add_argument("--tile", type=int, default=256)
+    ap.add_argument("--storage", choices=["f64", "f32"], default="f64",
+                    help="matrix element type (arithmetic is fp64 either way; f32 = BASELINE configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=6144)
     args = ap.parse_args()
@@ -132,7 +134,7 @@ def main():
     m = args.rows or (16384 if world == 1 else 65536)
     n = args.cols or 16384
     b = args.tile
-    dt = torch.float64
+    dt = torch.float64 if args.storage == "f64" else torch.float32
     q = n // b
 
     A0 = torch.empty((n, m), dtype=dt, device="cuda")
@@ -204,6 +206,8 @@ def main():
         cpu = cpu_baseline(args.cpu_sample, b)
 
     cfg = 2 if (m, n) == (16384, 16384) else 3 if (m, n) == (65536, 16384) else 1 if (m, n) == (4096, 4096) else "custom"
+    if args.storage == "f32":
+        cfg = 4 if (m, n) == (32768, 32768) else "custom"
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -218,7 +222,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (RANDZO distribution, device-generated)",
-            "config": {"workload": f"tiled QR {m}x{n} fp64, tile {b} (BASELINE configs[{cfg}])", "m": m, "n": n,
+            "config": {"workload": f"tiled QR {m}x{n} {args.storage} storage, tile {b} (BASELINE configs[{cfg}])", "m": m, "n": n,
                        "tile": b, "parallelism": "single GPU" if world == 1 else
                        f"{world} GPUs, tile-column cyclic, panel V/T forwarded over xGMI"},
             "roofline": roof,

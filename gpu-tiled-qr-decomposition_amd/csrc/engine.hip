@@ -338,6 +338,8 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
   // cost model (unit: one chain element): Tg = one panel group-step; tunable for experiments
   const char* eg = getenv("TQR_TG");
   const double Tg = eg ? atof(eg) : 1.4, Te = 1.0;
+  const char* el = getenv("TQR_LAZY");
+  const double lazy = el ? atof(el) : 1.0;
   // fin_elem[k][i][j] (strips move together in the estimate): finish of chain element (i,j,k)
   auto id3 = [&](int k, int i, int j) { return ((size_t)k * p + i) * q + j; };
   std::vector<double> fin((size_t)kmax * p * q, 0.0), pstart((size_t)kmax * p, 0.0);
@@ -372,8 +374,14 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
       for (int e = 0; e < nseg; ++e) {
         int i0 = k + 1 + e * seglen, i1 = std::min(p, i0 + seglen);
         if (p - k - 1 == 0) { i0 = p; i1 = p; }
+        // lazy keys (TQR_LAZY, default 1): a segment of a non-lookahead column is keyed by the
+        // estimated completion of its first panel member, so a workgroup does not dequeue it
+        // long before its V/T images exist (it would wait group by group); the lookahead
+        // column k+1 feeds the next panel and stays eager
+        double key = seg_start[std::min<size_t>(e, seg_start.size() - 1)];
+        if (lazy > 0 && j != k + 1 && i0 < p) key = std::max(key, pstart[(size_t)k * p + i0] + lazy * ng * Tg);
         for (int s = 0; s < ns; ++s)
-          tl.push_back({seg_start[std::min<size_t>(e, seg_start.size() - 1)], 1,
+          tl.push_back({key, 1,
                         Item{T_CHAIN | (s << 8), i0 | (i1 << 16), j, k | (e << 16)}});
       }
     }
@@ -542,7 +550,7 @@ struct tqr_plan {
   int engine = 1;          // 1 = persistent dataflow (default), 0 = wave-batched launches
   Item* d_flow = nullptr;
   int nflow = 0;
-  int* d_sync = nullptr;   // next, err, Rc, Tc, Ac, Rt
+  int* d_sync = nullptr;   // next, err, Rc, Tc, Ac, Rt, Rr
   size_t sync_ints = 0;
   int ns = 1, ng = 1, grid = 256, est_order = 0;
   ffn kflow = nullptr;
@@ -555,8 +563,7 @@ struct tqr_plan {
   // multi-GPU (tile-column cyclic partition): rank / world, uncached panel counters, forward
   // counters, peer workspaces opened by IPC
   int rank = 0, world = 1;
-  int* d_rc = nullptr;
-  int* d_fc = nullptr;
+  int* d_rf = nullptr;     // multi-GPU member flags (uncached), kmax x p x ng
   PeerBufs* d_peers = nullptr;
   double** d_peer_wk = nullptr;  // world x kmax opened peer workspace pointers
   std::vector<void*> opened;     // IPC-opened peer pointers
@@ -624,8 +631,7 @@ void tqr_plan_destroy(tqr_plan* pl) {
   for (void* p : pl->opened) (void)hipIpcCloseMemHandle(p);
   if (pl->d_peers) (void)hipFree(pl->d_peers);
   if (pl->d_peer_wk) (void)hipFree(pl->d_peer_wk);
-  if (pl->d_rc) (void)hipFree(pl->d_rc);
-  if (pl->d_fc) (void)hipFree(pl->d_fc);
+  if (pl->d_rf) (void)hipFree(pl->d_rf);
   delete pl;
 }
 
@@ -710,7 +716,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
-    pl->sync_ints = 2 + 2 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns + (size_t)pl->kmax * pl->q * pl->ns;
+    pl->sync_ints = 2 + 3 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns + (size_t)pl->kmax * pl->q * pl->ns;
     if (pl->nflow <= 0 || hipMalloc(&pl->d_flow, sizeof(Item) * pl->nflow) != hipSuccess ||
         hipMalloc(&pl->d_sync, sizeof(int) * pl->sync_ints) != hipSuccess ||
         hipMalloc(&pl->d_wk, sizeof(double*) * pl->kmax) != hipSuccess) {
@@ -729,10 +735,10 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
       tqr_plan_destroy(pl); return TQR_EHIP;
     }
     if (world > 1) {
-      // panel counters in uncached memory (peers' forward tasks add to them over xGMI)
-      const size_t nrc = sizeof(int) * (size_t)pl->kmax * pl->ng;
-      if (hipExtMallocWithFlags((void**)&pl->d_rc, nrc, hipDeviceMallocUncached) != hipSuccess ||
-          hipMalloc(&pl->d_fc, nrc) != hipSuccess || hipMalloc(&pl->d_peers, sizeof(PeerBufs) * world) != hipSuccess ||
+      // member flags in uncached memory (peers' forward tasks set them over xGMI)
+      const size_t nrf = sizeof(int) * (size_t)pl->kmax * pl->p * pl->ng;
+      if (hipExtMallocWithFlags((void**)&pl->d_rf, nrf, hipDeviceMallocUncached) != hipSuccess ||
+          hipMalloc(&pl->d_peers, sizeof(PeerBufs) * world) != hipSuccess ||
           hipMalloc(&pl->d_peer_wk, sizeof(double*) * (size_t)world * pl->kmax) != hipSuccess) {
         tqr_plan_destroy(pl); return TQR_ENOMEM;
       }
@@ -776,7 +782,7 @@ size_t tqr_dist_handle_bytes(const tqr_plan* pl) {
 int tqr_dist_export(tqr_plan* pl, void* buf, size_t len) {
   if (!pl || pl->world < 2 || !buf || len < tqr_dist_handle_bytes(pl)) return TQR_EINVAL;
   std::vector<hipIpcMemHandle_t> h(1 + pl->kmax);
-  HIPCHK(hipIpcGetMemHandle(&h[0], pl->d_rc));
+  HIPCHK(hipIpcGetMemHandle(&h[0], pl->d_rf));
   for (int k = 0; k < pl->kmax; ++k) HIPCHK(hipIpcGetMemHandle(&h[1 + k], pl->wk[k]));
   memcpy(buf, h.data(), sizeof(hipIpcMemHandle_t) * h.size());
   return TQR_OK;
@@ -791,7 +797,7 @@ int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
     double** tab = pl->d_peer_wk + (size_t)r * pl->kmax;
     if (r == pl->rank) {
       for (int k = 0; k < pl->kmax; ++k) pwk[(size_t)r * pl->kmax + k] = pl->wk[k];
-      pb[r] = PeerBufs{tab, pl->d_rc};
+      pb[r] = PeerBufs{tab, pl->d_rf};
       continue;
     }
     std::vector<hipIpcMemHandle_t> h(1 + pl->kmax);
@@ -803,7 +809,7 @@ int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
         return TQR_EHIP;
       }
       pl->opened.push_back(p);
-      if (x == 0) pb[r].Rc = (int*)p;
+      if (x == 0) pb[r].Rf = (int*)p;
       else pwk[(size_t)r * pl->kmax + x - 1] = (double*)p;
     }
     pb[r].Wk = tab;
@@ -817,8 +823,7 @@ int tqr_dist_reset(tqr_plan* pl, void* stream) {
   if (!pl || pl->world < 2) return TQR_EINVAL;
   hipStream_t cs = (hipStream_t)stream;
   HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
-  HIPCHK(hipMemsetAsync(pl->d_rc, 0, sizeof(int) * (size_t)pl->kmax * pl->ng, cs));
-  HIPCHK(hipMemsetAsync(pl->d_fc, 0, sizeof(int) * (size_t)pl->kmax * pl->ng, cs));
+  HIPCHK(hipMemsetAsync(pl->d_rf, 0, sizeof(int) * (size_t)pl->kmax * pl->p * pl->ng, cs));
   return TQR_OK;
 }
 
@@ -886,9 +891,10 @@ int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream)
     f.Tc = f.Rc + (size_t)pl->kmax * pl->ng;
     f.Ac = f.Tc + (size_t)pl->p * pl->q * pl->ns;
     f.Rt = f.Ac + (size_t)pl->kmax * pl->q * pl->ns;
-    f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.peers = pl->d_peers; f.Fc = pl->d_fc;
-    if (pl->world > 1) f.Rc = pl->d_rc;  // counters reset by tqr_dist_reset (all ranks, then a barrier)
-    else HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
+    f.Rr = f.Rt + (size_t)pl->kmax * pl->ng;
+    f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.peers = pl->d_peers; f.Rf = pl->d_rf;
+    // multi-GPU: counters and flags are reset by tqr_dist_reset (all ranks, then a barrier)
+    if (pl->world == 1) HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
     if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
     hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(FLOW_NT), pl->ldsF, cs, f);
     HIPCHK(hipGetLastError());

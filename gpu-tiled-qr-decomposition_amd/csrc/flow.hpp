@@ -10,6 +10,9 @@
 //                   UNMQR(k,j) (segment 0 only), TSMQR(i,j,k) for i in [i0,i1). The strip of
 //                   tile (k,j) (the TSMQR head rows) stays owned by the chain across elements.
 // Progress counters (zeroed per factorisation):
+//   Rr[k][g]   members of panel k whose group-g factorisation (R diagonal block, V, tau) is in
+//              memory — all the next member's factorisation of group g needs; build_t, the
+//              images and the trailing update come after it, off the member-to-member path;
 //   Rt[k][g]   members of panel k that finished the in-tile trailing update of group g (the R_kk
 //              head rows of the group's columns right of it): the next member's trailing update
 //              waits for it, its factorisation of group g does not (it needs only the 32 x 32
@@ -66,7 +69,7 @@ constexpr unsigned long long FLOW_TIMEOUT = 500000000ull;  // 5 s of s_memrealti
 // Multi-GPU (tile-column cyclic partition, one process per GPU): peer buffers opened by IPC.
 struct PeerBufs {
   double* const* Wk;  // the peer's panel workspaces (IPC-opened into this process), one per k
-  int* Rc;
+  int* Rf;            // the peer's member flags
 };
 
 struct FlowArgs {
@@ -85,11 +88,13 @@ struct FlowArgs {
   int* Tc;
   int* Ac;
   int* Rt;
-  // multi-GPU: dist = world > 1. Rc then lives in uncached memory written by peers' forward
-  // tasks over xGMI and is accessed at system scope; Fc[k][g] orders this rank's forwards.
+  int* Rr;
+  // multi-GPU: dist = world > 1. Rf[k][i][g] (uncached memory) = 1 once the owner of panel k
+  // forwarded the V/T images of member i, group g into this rank's workspace (set by the peer
+  // over xGMI, polled at system scope). Panel counters Rc/Rr/Rt stay local to the owner.
   int dist, rank, world;
   const PeerBufs* peers;
-  int* Fc;
+  int* Rf;
 };
 
 // ---- synchronisation ---------------------------------------------------------------------
@@ -296,7 +301,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     const int c0 = g * IB, ks0 = c0 / 4;
     if (!qrs) {  // R_kk rows of group g as left by the previous chain member
       FST(5);
-      const bool ok = t == 0 ? spin_ge(&a.Rc[(size_t)k * NG + g], pos, a.err, a.dist) : true;
+      const bool ok = t == 0 ? spin_ge(&a.Rr[(size_t)k * NG + g], pos, a.err) : true;
       if (!wg_verdict(ok, sflag)) return;
       FST(1);
     }
@@ -336,7 +341,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       }
     }
     if (t < IB) st(tau + (size_t)k * a.m + (size_t)(qrs ? k : l) * B + c0 + t, tauv[t]);
-    __syncthreads();
+    wg_publish(&a.Rr[(size_t)k * NG + g], 1);  // includes the drain and the barrier
     if (qrs) {
       for (int idx = t; idx < B * IB; idx += FLOW_NT) {
         const int r = idx % B, c = idx / B, d = c0 + c;
@@ -352,7 +357,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       for (int idx = t; idx < G::VSZ; idx += FLOW_NT) st(vg + idx, Vs[vimg_row(idx / VP) * VP + idx % VP]);
     }
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
-    wg_publish(&a.Rc[(size_t)k * NG + g], 1, a.dist);
+    wg_publish(&a.Rc[(size_t)k * NG + g], 1);
     if (!qrs) {  // R_kk head rows right of the group as left by the previous member's trailing
       FST(5);
       const bool ok = t == 0 ? spin_ge(&a.Rt[(size_t)k * NG + g], pos, a.err) : true;
@@ -381,11 +386,12 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
 }
 
 // ---- forward tasks (multi-GPU) -------------------------------------------------------------
-// FWD(i,k) on the owner of panel k: group by group, once member i finished group g here and
-// FWD(i-1,k) forwarded group g (Fc, so every peer counter advances member by member), copy the
-// V and T images of (i,k,g) into every peer's workspace with system-scope (sc0 sc1) 16-B
-// stores over xGMI, drain, release at system scope, and bump each peer's Rc[k][g]. Peers' chains
-// then LDS-DMA the images from their own HBM exactly as the owner's chains do.
+// FWD(i,k) on the owner of panel k: group by group, once member i finished group g here, copy the
+// V and T images of (i,k,g) into every peer's workspace with system-scope (sc0 sc1) 16-B stores
+// over xGMI, drain, release at system scope, and set each peer's flag Rf[k][i][g]. Peers' chains
+// then LDS-DMA the images from their own HBM exactly as the owner's chains do. Per-member flags
+// (not counters) let the forwards of different members run concurrently on different
+// workgroups: a panel's images leave as fast as they are produced.
 template <int B>
 __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sflag) {
   using G = Geo<B>;
@@ -393,7 +399,7 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
   const int t = threadIdx.x, pos = i - k;
   for (int g = 0; g < NG; ++g) {
     bool ok = true;
-    if (t == 0) ok = spin_ge(&a.Rc[(size_t)k * NG + g], pos + 1, a.err, true) && spin_ge(&a.Fc[(size_t)k * NG + g], pos, a.err);
+    if (t == 0) ok = spin_ge(&a.Rc[(size_t)k * NG + g], pos + 1, a.err);
     if (!wg_verdict(ok, sflag)) return;
     const size_t vo = flow_vw_off<B>(a.p, i, k, g), to = flow_tw_off<B>(a.p, i, k, g);
     const __amdgpu_buffer_rsrc_t vsrc = uniform_rsrc(a.Wk[k] + vo), tsrc = uniform_rsrc(a.Wk[k] + to);
@@ -410,10 +416,9 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
     __syncthreads();
     if (t == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+      const size_t fo = ((size_t)k * a.p + i) * NG + g;
       for (int r = 0; r < a.world; ++r)
-        if (r != a.rank) __hip_atomic_fetch_add(&a.peers[r].Rc[(size_t)k * NG + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // peer increments performed before ours
-      __hip_atomic_fetch_add(&a.Fc[(size_t)k * NG + g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (r != a.rank) __hip_atomic_store(&a.peers[r].Rf[fo], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
   }
@@ -452,6 +457,17 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
   PanelView<NG> pv;
   pv.init(sflag + 48);
   int tc_pf = -1;  // thread 0: Tc of the next element's tile, loaded one group ahead
+  // multi-GPU, panel owned by another rank: per-member flags forwarded by the owner
+  const bool remote = a.dist && (k % a.world != a.rank);
+  int* const rf = a.Rf + (size_t)k * a.p * NG;
+  int* fl_pf = nullptr;  // thread 0: the flag the next sync point tests, and its early load
+  int fl_pv = 0;
+  auto ready = [&](int i_, int g_) -> bool {
+    if (!remote) return pv.ensure(rc, g_, i_ - k + 1, a.err, false);
+    int* fp = rf + (size_t)i_ * NG + g_;
+    if (fp == fl_pf && fl_pv >= 1) return true;
+    return spin_ge(fp, 1, a.err, true);
+  };
   FST(6);
   const int ifirst = seg == 0 ? k : i0;
   for (int i = ifirst; i < i1 || i == k; i = (i == k ? i0 : i + 1)) {
@@ -465,7 +481,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
         if (ok && k > 0 && tc_pf < k) ok = spin_ge(tc(i), k, a.err);
         tc_pf = -1;
         FST(8);
-        if (ok && !dma_next) ok = pv.ensure(rc, 0, need, a.err, a.dist);
+        if (ok && !dma_next) ok = ready(i, 0);
       }
       FST(0);
       if (!sync_point<false>(ok, sflag, par)) return;
@@ -491,8 +507,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
       {
         bool ok = true;
         if (t == 0) {
-          if (g + 1 < NG) ok = pv.ensure(rc, g + 1, need, a.err, a.dist);
-          else if (has_next) ok = pv.ensure(rc, 0, inext - k + 1, a.err, a.dist);
+          if (g + 1 < NG) ok = ready(i, g + 1);
+          else if (has_next) ok = ready(inext, 0);
         }
         FST(0);
         if (!sync_point<true>(ok, sflag, par)) return;
@@ -502,7 +518,12 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
         pending = nullptr;
       }
       if (t == 0) {  // early loads of the counters the next sync point will test
-        pv.prefetch(rc, a.dist);
+        if (!remote) {
+          pv.prefetch(rc, false);
+        } else {
+          fl_pf = g + 1 < NG ? rf + (size_t)i * NG + g + 1 : has_next ? rf + (size_t)inext * NG : nullptr;
+          fl_pv = fl_pf ? ld_sys(fl_pf) : 0;
+        }
         if (g + 1 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
       }
       FST(7);

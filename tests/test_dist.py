@@ -3,9 +3,9 @@
 CPU (no GPU): every rank's task list is the global list restricted to its tile columns plus
 one forward task per owned panel member — checked for world sizes 1-8 and inside a world-2
 gloo process group (as the bench's ranks build them).
-GPU: two ranks on ONE device (the box has one GPU), each with half the CUs, run the real
-protocol — IPC-opened peer workspaces, forward tasks, uncached counters — and must reproduce
-the single-GPU engine bit for bit (the per-tile operation sequence is the same).
+GPU: two or four ranks on ONE device (the box has one GPU), each with a share of the CUs, run the
+real protocol — IPC-opened peer workspaces, forward tasks, uncached member flags — and must
+reproduce the single-GPU engine bit for bit (the per-tile operation sequence is the same).
 """
 import json
 import os
@@ -78,12 +78,13 @@ def test_partition_gloo_world2():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("m,n,b,dt", [(1024, 1024, 128, "f64"), (2048, 768, 256, "f64"), (512, 1024, 64, "f64"),
-                                      (1024, 512, 128, "f32")])
-def test_two_ranks_one_gpu_match_single_gpu(m, n, b, dt):
-    env = dict(os.environ, TQR_FLOW_GRID="96")
+@pytest.mark.parametrize("m,n,b,dt,ranks", [(1024, 1024, 128, "f64", 2), (2048, 768, 256, "f64", 2),
+                                            (512, 1024, 64, "f64", 2), (1024, 512, 128, "f32", 2),
+                                            (2048, 2048, 256, "f64", 4)])
+def test_ranks_on_one_gpu_match_single_gpu(m, n, b, dt, ranks):
+    env = dict(os.environ, TQR_FLOW_GRID=str(192 // ranks))
     port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr=127.0.0.1", f"--master-port={port}",
            os.path.join(HERE, "dist_worker.py"), str(m), str(n), str(b), dt, "0"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
