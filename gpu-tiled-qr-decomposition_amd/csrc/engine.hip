@@ -59,11 +59,12 @@ __device__ unsigned long long g_pstamps[8];
 #endif
 
 #ifdef TQR_FLOW_STAMPS
-__device__ unsigned long long g_fst[4096 * 12];
+__device__ unsigned long long g_fst[4096 * 16];  // >= FST_N categories per workgroup
 #endif
 }  // namespace tqr
 #include "flow.hpp"
 namespace tqr {
+static_assert(FST_N <= 16, "g_fst holds 16 categories per workgroup");
 
 template <int B>
 __device__ __forceinline__ double* tw_ptr(const Args& a, int i, int k, int g) {

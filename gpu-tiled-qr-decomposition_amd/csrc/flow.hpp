@@ -39,8 +39,9 @@ constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel memb
 // thread 0 only, written to g_fst[blockIdx.x][*] at exit). Categories: 0 chain waits,
 // 1 panel waits, 2 chain head-row I/O, 3 chain apply (with the LDS-DMA issue), 4 chain strip
 // I/O + publish, 5 panel compute, 6 dequeue/dispatch + kernel exit, 7 chain drain + barrier,
-// 8 chain Tc waits (tile's previous step), 9 chain Ac waits (previous segment).
-constexpr int FST_N = 12;
+// 8 chain Tc waits (tile's previous step), 9 chain Ac waits (previous segment), 10 panel I/O +
+// writeback + images, 11 panel build_t, 12 panel in-tile trailing update (+ its Rt publish).
+constexpr int FST_N = 13;
 #ifdef TQR_FLOW_STAMPS
 extern __device__ unsigned long long g_fst[];
 #define FST(c)                                                                            \
@@ -300,7 +301,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
   for (int g = 0; g < NG; ++g) {
     const int c0 = g * IB, ks0 = c0 / 4;
     if (!qrs) {  // R_kk rows of group g as left by the previous chain member
-      FST(5);
+      FST(10);
       const bool ok = t == 0 ? spin_ge(&a.Rr[(size_t)k * NG + g], pos, a.err) : true;
       if (!wg_verdict(ok, sflag)) return;
       FST(1);
@@ -323,8 +324,10 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       }
     }
     __syncthreads();
+    FST(10);
     if (qrs) panel_factor<B, false>(Vs, Hs, tauv, scratch, c0);
     else panel_factor<B, true>(Vs, Hs, tauv, scratch, c0);
+    FST(5);
     if (qrs) {
       for (int idx = t; idx < B * IB; idx += FLOW_NT) {
         const int r = idx % B, c = idx / B;
@@ -349,7 +352,9 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       }
       __syncthreads();
     }
+    FST(10);
     build_t<B>(Vs, tauv, Gs, Ts, Gp, qrs ? ks0 : 0);
+    FST(11);
     {  // V image (explicit) and T image of this group for the chains (LDS-DMA sources)
       double* tg = flow_tw<B>(a, qrs ? k : l, k, g);
       double* vg = flow_vw<B>(a, qrs ? k : l, k, g);
@@ -358,8 +363,8 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     }
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
     wg_publish(&a.Rc[(size_t)k * NG + g], 1);
+    FST(10);
     if (!qrs) {  // R_kk head rows right of the group as left by the previous member's trailing
-      FST(5);
       const bool ok = t == 0 ? spin_ge(&a.Rt[(size_t)k * NG + g], pos, a.err) : true;
       if (!wg_verdict(ok, sflag)) return;
       FST(1);
@@ -381,8 +386,8 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       }
     }
     wg_publish(&a.Rt[(size_t)k * NG + g], 1);
+    FST(12);
   }
-  FST(5);
 }
 
 // ---- forward tasks (multi-GPU) -------------------------------------------------------------

@@ -471,109 +471,98 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return dbl_of(lo, hi);
 }
 
-// One reflector step; C is a template parameter so x[C] and the j-windows are static (a
-// runtime c would force x[] into scratch memory).
-//   1. every tail row forms x_C * x_j (j in the live window) and the wave reduce-scatters them;
+// One reflector step, as a loop body over a shifting window (the code stays a few KiB: a fully
+// unrolled 32-step panel was 60 KiB of straight-line code per variant, streamed through the
+// instruction cache on every call — 70 us per group in the persistent engine instead of ~35).
+// Thread t holds row t of the live columns in x[0..NW): x[jr] = column C + jr; finished columns
+// are written to the V image and shifted out, zeros shift in.
+//   1. every tail row forms x_C * x_j (j in the window) and the wave reduce-scatters them;
 //   2. one barrier; each lane sums the 4 wave partials of "its" column j and reads head_j;
 //   3. the pivot's D_C and head_C are read from the owning lane (s_readlane, uniform);
 //   4. lane of column j forms f_j = tau (head_j + scale D_j) and publishes it wave-privately;
 //   5. rows update x_j -= f_j v (tails) / head_j -= f_j (GE head row, TS head in `hout`).
-template <int B, bool TS, int C>
-__device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Hs, double* tauv, double* red, double* wb,
-                                           double* hrow, double* hout, int c0, bool own, int mycol, bool writer) {
+template <int B, bool TS, int NW>
+__device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, double* Hs, double* tauv, double* red,
+                                           double* wb, double* hrow, double* hout, int c0, int C, bool own) {
   using g = Geo<B>;
-  constexpr int IB = g::IB, TP = g::TP;
+  constexpr int IB = g::IB, TP = g::TP, VP = g::VP;
+  constexpr int SPAN = 64 / NW;  // lanes holding the same column after reduce-scatter
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int rc = c0 + C;  // GE: tile row of the reflector head
   const bool tail = own && (TS || t > rc);
-  PSTAMP_INIT
-  // reduce only the live window j >= C: 32 wide, or the upper 16 once C >= 16
-  constexpr int NW = (IB == 32 && C >= 16) ? 16 : IB;
-  constexpr int J0 = IB - NW;
-  constexpr int SPAN = 64 / NW;          // lanes holding the same column after reduce-scatter
-  constexpr int LC = (C - J0) * SPAN;    // a lane holding column C (rs_col is lane / SPAN)
   double pv[NW];
 #pragma unroll
-  for (int j = 0; j < NW; ++j) pv[j] = (J0 + j >= C && tail) ? x[C] * x[J0 + j] : 0.0;
+  for (int j = 0; j < NW; ++j) pv[j] = tail ? x[0] * x[j] : 0.0;
   const double ws = RS<NW>::run(pv, lane);
-  const int cw = J0 + rs_col<NW>(lane);
+  const int cr = rs_col<NW>(lane);  // relative column of this lane's sum
+  const int cw = C + cr;            // absolute column (>= IB: outside the panel, ignored)
   const bool wr = (lane & (SPAN - 1)) == 0;
   double* rb = red + (C & 1) * 128;
-  if (wr && w < 4) rb[w * 32 + cw] = ws;  // rows live in waves 0-3 (a 512-thread workgroup's 4-7 idle)
+  if (wr && w < 4) rb[w * 32 + cr] = ws;  // rows live in waves 0-3
   if (!TS && t == rc) {
 #pragma unroll
-    for (int j = C; j < IB; ++j) hrow[(C & 1) * 32 + j] = x[j];
+    for (int j = 0; j < NW; ++j) hrow[(C & 1) * 32 + j] = x[j];
   }
-  PSTAMP(0);
   __syncthreads();
-  PSTAMP(1);
-  const double* Hh = TS ? (Hs + C * TP) : (hrow + (C & 1) * 32);
-  const double Dm = (rb[cw] + rb[32 + cw]) + (rb[64 + cw] + rb[96 + cw]);
-  const double Hm = Hh[cw];
-  const double dc = readlane_d(Dm, LC);
-  const double x0 = readlane_d(Hm, LC);
+  const double Dm = (rb[cr] + rb[32 + cr]) + (rb[64 + cr] + rb[96 + cr]);
+  const double Hm = TS ? (cw < IB ? Hs[C * TP + cw] : 0.0) : hrow[(C & 1) * 32 + cr];
+  const double dc = readlane_d(Dm, 0);
+  const double x0 = readlane_d(Hm, 0);
   const double norm = sqrt(x0 * x0 + dc);
   const double hd = x0 + (x0 >= 0.0 ? norm : -norm);
   const double scale = norm != 0.0 ? rcp_nr(hd) : 1.0;
   const double tau = 2.0 * rcp_nr(fma(scale * scale, dc, 1.0));
-  const double fm = tau * fma(scale, Dm, Hm);  // f_j for j = cw
+  const double fm = cw < IB ? tau * fma(scale, Dm, Hm) : 0.0;  // f_j for j = cw
   double* fb = wb + (w & 3) * 32;
-  if (wr && w < 4) fb[cw] = fm;
-  if (TS && w == 0 && wr && cw >= C) hout[C * TP + cw] = Hm - fm;  // cw == C: R_CC = x0 - f_C
+  if (wr && w < 4) fb[cr] = fm;
+  if (TS && w == 0 && wr && cw < IB) hout[C * TP + cw] = Hm - fm;  // cw == C: R_CC = x0 - f_C
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   double f[NW];
 #pragma unroll
   for (int h = 0; h < NW / 2; ++h) {
-    const double2 v2 = reinterpret_cast<const double2*>(fb + J0)[h];
+    const double2 v2 = reinterpret_cast<const double2*>(fb)[h];
     f[2 * h] = v2.x;
     f[2 * h + 1] = v2.y;
   }
-  PSTAMP(2);
   if (tail) {
-    const double xc = x[C] * scale;
+    const double xc = x[0] * scale;
 #pragma unroll
-    for (int j = C + 1; j < IB; ++j) x[j] = fma(-f[j - J0], xc, x[j]);
-    x[C] = xc;
+    for (int j = 1; j < NW; ++j) x[j] = fma(-f[j], xc, x[j]);
+    x[0] = xc;
   } else if (!TS && t == rc) {
 #pragma unroll
-    for (int j = C + 1; j < IB; ++j) x[j] -= f[j - J0];
-    x[C] = x0 - f[C - J0];
+    for (int j = 1; j < NW; ++j) x[j] -= f[j];
+    x[0] = x0 - f[0];
   }
   if (t == 0) tauv[C] = tau;
-  PSTAMP(3);
+  // column C is final (V entry / R entry): out to the image, shift the window
+  if (own) Vs[t * VP + g::pc(C)] = x[0];
+#pragma unroll
+  for (int j = 0; j + 1 < NW; ++j) x[j] = x[j + 1];
+  x[NW - 1] = 0.0;
 }
 
-template <int B, bool TS, int C>
-struct PanelSteps {
-  __device__ static __forceinline__ void run(double (&x)[Geo<B>::IB], double* Hs, double* tauv, double* red, double* wb,
-                                             double* hrow, double* hout, int c0, bool own, int mycol, bool writer) {
-    if constexpr (C < Geo<B>::IB) {
-      panel_step<B, TS, C>(x, Hs, tauv, red, wb, hrow, hout, c0, own, mycol, writer);
-      PanelSteps<B, TS, C + 1>::run(x, Hs, tauv, red, wb, hrow, hout, c0, own, mycol, writer);
-    }
-  }
-};
-
 template <int B, bool TS>
-__device__ void panel_factor(double* Vs, double* Hs, double* tauv, double* scratch, int c0) {
+__device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, double* scratch, int c0) {
   using g = Geo<B>;
   constexpr int IB = g::IB, VP = g::VP, TP = g::TP;
   double* red = scratch;             // 2 x [4 waves][32] cross-wave partials (double-buffered)
   double* wb = red + 2 * 4 * 32;     // [4 waves][32] per-wave totals
   double* hrow = wb + 4 * 32;        // 2 x [32] GE head row broadcast (double-buffered)
   double* hout = hrow + 2 * 32;      // [IB][TP] TS updated head rows
-  const int t = threadIdx.x, lane = t & 63;
+  const int t = threadIdx.x;
   const bool own = t < B && (TS || t >= c0);
   double x[IB];
 #pragma unroll
   for (int j = 0; j < IB; ++j) x[j] = own ? Vs[t * VP + g::pc(j)] : 0.0;
-  const int mycol = rs_col<IB>(lane);
-  const bool writer = (lane & (64 / IB - 1)) == 0;
-  PanelSteps<B, TS, 0>::run(x, Hs, tauv, red, wb, hrow, hout, c0, own, mycol, writer);
-  if (own) {
-#pragma unroll
-    for (int j = 0; j < IB; ++j) Vs[t * VP + g::pc(j)] = x[j];
+  // reduce the live window only: all IB columns while more than IB/2 are live, then the half
+  constexpr int HALF = IB == 32 ? 16 : IB;
+#pragma clang loop unroll(disable)
+  for (int C = 0; C < HALF; ++C) panel_step<B, TS, IB>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own);
+  if constexpr (HALF < IB) {
+#pragma clang loop unroll(disable)
+    for (int C = HALF; C < IB; ++C) panel_step<B, TS, IB / 2>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own);
   }
   __syncthreads();
   if (TS) {
@@ -595,7 +584,7 @@ __device__ void panel_factor(double* Vs, double* Hs, double* tauv, double* scrat
 // Gs, Ts: IB x TP images. ks0: first non-zero 4-row block of V (GE), 0 for TS.
 // ---------------------------------------------------------------------------------------
 template <int B>
-__device__ void build_t(const double* Vs, const double* tauv, double* Gs, double* Ts, double* Gp, int ks0) {
+__device__ __noinline__ void build_t(const double* Vs, const double* tauv, double* Gs, double* Ts, double* Gp, int ks0) {
   using g = Geo<B>;
   constexpr int IB = g::IB, VP = g::VP, TP = g::TP, NKS = g::NKS, NRI = g::NRI;
   constexpr int KPW = (NKS + 3) / 4;  // k-steps per wave

@@ -20,14 +20,19 @@ for rep in range(2):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
 nb = torch.cuda.get_device_properties(0).multi_processor_count
-NC = 12
+NC = 13
 st = (ctypes.c_ulonglong * (NC * nb))()
 assert L.tqr_debug_flow_stamps(st, nb) == 0
 names = ["chain Rc polls (thread 0)", "panel waits", "chain head-row I/O", "chain apply (+DMA issue)",
-         "chain strip I/O+publish", "panel compute", "dequeue/dispatch/exit", "chain drain+barrier",
-         "chain Tc waits", "chain Ac waits", "-", "-"]
+         "chain strip I/O+publish", "panel_factor", "dequeue/dispatch/exit", "chain drain+barrier",
+         "chain Tc waits", "chain Ac waits", "panel I/O+images", "panel build_t", "panel trailing update"]
 tot = [sum(st[w * NC + c] for w in range(nb)) for c in range(NC)]
 allt = sum(tot)
 print(f"{m}x{n} b={b}: wall {ms:.1f} ms; {nb} workgroups; sum of stamps {allt / nb / 1e5:.1f} ms per WG")
-for c in range(10):
+p, q = m // b, n // b
+npanel = sum(p - k for k in range(min(p, q)))
+ng = b // 32
+for c, nm in ((5, "panel_factor"), (11, "build_t"), (12, "trailing"), (10, "panel I/O")):
+    print(f"  per panel group ({npanel * ng} groups): {nm:14s} {tot[c] / (npanel * ng) / 100:7.2f} us")
+for c in range(NC):
     print(f"  {names[c]:24s} {tot[c] / nb / 1e5:8.2f} ms/WG  {100.0 * tot[c] / allt:5.1f}%")
