@@ -184,21 +184,33 @@ struct DmaJob {
   double* dst;
   const double* v;
   const double* t;
-  bool on;
+  // Branch-free: every wave issues exactly STEPS instructions (a wave past the end of an image
+  // re-copies its last KiB — identical bytes to the same LDS words), and a job with nothing to
+  // fetch is pointed by the caller at an image it may legally re-read into the idle buffer.
+  // Control flow inside the MFMA stream made the compiler drop its partial lgkmcnt waits.
   __device__ __forceinline__ void step(int m) const {
-    if (!on) return;
     // wave id made provably uniform: addresses = scalar base + one per-lane offset register
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (m < PV) {
-      const int u = w + FLOW_NW * m;
-      if (u < NIV)
-        __builtin_amdgcn_global_load_lds((glb_void_t*)(v + u * 128 + 2 * lane), (lds_void_t*)(dst + u * 128), 16, 0, 16);
+      const int u = min(w + FLOW_NW * m, NIV - 1);
+      dma16(v + u * 128 + 2 * lane, dst + u * 128);
     } else if (m < STEPS) {
-      const int u = w + FLOW_NW * (m - PV);
-      if (u < NIT)
-        __builtin_amdgcn_global_load_lds((glb_void_t*)(t + u * 128 + 2 * lane),
-                                         (lds_void_t*)(dst + Geo<B>::VIMG + u * 128), 16, 0, 16);
+      const int u = min(w + FLOW_NW * (m - PV), NIT - 1);
+      dma16(t + u * 128 + 2 * lane, dst + Geo<B>::VIMG + u * 128);
     }
+  }
+  // One wave-wide 16-B-per-lane LDS-DMA (1 KiB, lane-linear at lds_wave). Issued as inline asm:
+  // for the builtin the compiler cannot tell the DMA's LDS destination (the idle buffer) from the
+  // operand reads of the buffer in use, and drains every outstanding ds_read (lgkmcnt(0)) before
+  // each DMA, which unpipelines the MFMA stream. Completion is tracked by hand: every consumer
+  // sits behind sync_point<true>'s explicit vmcnt(0); the compiler's own vmcnt accounting only
+  // over-waits when it does not see these (in-order counter), never under-waits.
+  static __device__ __forceinline__ void dma16(const double* src, double* lds_wave) {
+    const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void_t*)lds_wave);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(src), "s"(l) : "memory", "m0");
+#pragma clang diagnostic pop
   }
 };
 
@@ -449,7 +461,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
   const size_t ldm = a.ldm;
   const int t = threadIdx.x, w = t >> 6;
   const int col = s * FLOW_SW + 16 * w;  // this wave's 16 columns inside the tile
-  const bool active = col < B;
+  const bool active = B % FLOW_SW == 0 || col < B;  // (compile-time true unless B < FLOW_SW)
   S* At = A + (size_t)j * B * ldm + (size_t)k * B;  // tile (k,j): the chain's head rows
   int* const rc = &a.Rc[(size_t)k * NG];
   int* const ac = &a.Ac[((size_t)k * a.q + j) * a.ns + s];
@@ -493,21 +505,24 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
     }
     FST(7);
     S* Xt = ts ? A + (size_t)j * B * ldm + (size_t)i * B : At;
+#ifndef TQR_DIAG_NOSTRIP
     if (active) load_strip_pair<B, S>(X, Xt, ldm, col);
+#endif
     if (!dma_next) {
-      DmaJob<B> d{lds + buf * BUF, flow_vw<B>(a, i, k, 0), flow_tw<B>(a, i, k, 0), true};
+      DmaJob<B> d{lds + buf * BUF, flow_vw<B>(a, i, k, 0), flow_tw<B>(a, i, k, 0)};
       for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
     }
     dma_next = false;
-    // head rows: written by another workgroup before this segment (sc1 loads) or by this one
-    const bool first_ts = i == ifirst || i == k + 1;  // head rows last written by another workgroup
-    if (FLOW_PF && ts && active) {
-      if (first_ts) load_head<B, S, true>(H, At, ldm, 0, col);
-      else load_head<B, S, false>(H, At, ldm, 0, col);
-    }
+    // head rows: written by another workgroup before this segment or by this one (sc1 loads
+    // for both: one code path, no branch in the MFMA stream)
+    if (FLOW_PF && ts && active) load_head<B, S, true>(H, At, ldm, 0, col);
     FST(4);
     const int inext = (i == k) ? i0 : i + 1;
     const bool has_next = inext < i1;
+    // the group loop, unswitched on the element type (TSMQR / UNMQR) so that each copy is one
+    // straight MFMA stream with no per-group branches on the type
+    auto groups = [&](auto ts_c) -> bool {
+    constexpr bool ts = decltype(ts_c)::value;
     for (int g = 0; g < NG; ++g) {
       {
         bool ok = true;
@@ -516,7 +531,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
           else if (has_next) ok = ready(inext, 0);
         }
         FST(0);
-        if (!sync_point<true>(ok, sflag, par)) return;
+        if (!sync_point<true>(ok, sflag, par)) return false;
       }
       if (g == 0 && pending) {
         publish_after_drain(pending, 1);
@@ -532,39 +547,42 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
         if (g + 1 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
       }
       FST(7);
-      if (!FLOW_PF && ts && active) {  // two waves per SIMD: load the group's head rows here
-        if (first_ts) load_head<B, S, true>(H, At, ldm, g * IB, col);
-        else load_head<B, S, false>(H, At, ldm, g * IB, col);
-      }
+      if (!FLOW_PF && ts && active) load_head<B, S, true>(H, At, ldm, g * IB, col);  // 2 waves/SIMD
       const double* Vs = lds + buf * BUF;
       const double* Ts = Vs + G::VIMG;
       // the other buffer is free (every wave passed this sync point): next DMA rides phase 1
-      DmaJob<B> d{lds + (buf ^ 1) * BUF, nullptr, nullptr, false};
-      if (g + 1 < NG) {
-        d.v = flow_vw<B>(a, i, k, g + 1);
-        d.t = flow_tw<B>(a, i, k, g + 1);
-        d.on = true;
-      } else if (has_next) {
-        d.v = flow_vw<B>(a, inext, k, 0);
-        d.t = flow_tw<B>(a, inext, k, 0);
-        d.on = true;
-        dma_next = true;
+      // (nothing next: re-read this group's own images into the idle buffer, keeping the
+      // DMA stream branch-free)
+      const int gd = g + 1 < NG ? g + 1 : has_next ? 0 : g, id = g + 1 < NG ? i : has_next ? inext : i;
+      DmaJob<B> d{lds + (buf ^ 1) * BUF, flow_vw<B>(a, id, k, gd), flow_tw<B>(a, id, k, gd)};
+      dma_next = g + 1 == NG && has_next;
+#if defined(TQR_DIAG_DMA_FIXED)  // what-if: every DMA reads one L2-hot image
+      d.v = flow_vw<B>(a, k, k, 0);
+      d.t = flow_tw<B>(a, k, k, 0);
+#endif
+#ifdef TQR_DIAG_NODMA  // what-if: no staging at all
+      if (active) {
+        if (ts) apply_zw<B, true, NoHook, FLOW_PF>(Vs, Ts, X, H, W, 0);
+        else apply_zw<B, false, NoHook, FLOW_PF>(Vs, Ts, X, H, W, g * IB / 4);
       }
+#else
       if (active) {
         if (ts) apply_zw<B, true, DmaJob<B>, FLOW_PF>(Vs, Ts, X, H, W, 0, d);
         else apply_zw<B, false, DmaJob<B>, FLOW_PF>(Vs, Ts, X, H, W, g * IB / 4, d);
       } else {
         for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
       }
+#endif
       FST(3);
+#ifdef TQR_DIAG_NOHEAD
+      if (false) {
+#else
       if (ts && active) {
+#endif
         // head rows stay with this workgroup for the whole segment: plain (write-back) stores,
         // made visible to the next segment's workgroup by one release before the Ac publish
         store_head_plain<B>(H, At, ldm, g * IB, col);
-        if (FLOW_PF && g + 1 < NG) {
-          if (first_ts) load_head<B, S, true>(Hn, At, ldm, (g + 1) * IB, col);
-          else load_head<B, S, false>(Hn, At, ldm, (g + 1) * IB, col);
-        }
+        if (FLOW_PF && g + 1 < NG) load_head<B, S, true>(Hn, At, ldm, (g + 1) * IB, col);
       }
       FST(2);
       if (active) {
@@ -578,7 +596,12 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
       }
       buf ^= 1;
     }
+    return true;
+    };
+    if (!(ts ? groups(std::true_type{}) : groups(std::false_type{}))) return;
+#ifndef TQR_DIAG_NOSTRIP
     if (active) store_strip_pair<B, S>(X, Xt, ldm, col);
+#endif
     pending = tc(i);
     FST(4);
   }

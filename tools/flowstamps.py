@@ -4,7 +4,7 @@ import ctypes, os, sys, time
 import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpu-tiled-qr-decomposition_amd"))
 import tqr
-tqr.LIB_PATH = tqr.LIB_PATH.replace("libtqr.so", "libtqr_fst.so")
+tqr.LIB_PATH = tqr.LIB_PATH.replace("libtqr.so", os.environ.get("TQR_FST_LIB", "libtqr_fst.so"))
 L = tqr.lib()
 m = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 n = int(sys.argv[2]) if len(sys.argv) > 2 else m

@@ -217,8 +217,12 @@ __global__ __launch_bounds__(256, 1) void k_apply_dma(double* out, const double*
     asm volatile("" ::: "memory");
     const double* Vs = lds + buf * BUF;
     const double* src = img + (size_t)((it + blockIdx.x) % 512) * BUF;
-    DmaJob<B> d{lds + (buf ^ 1) * BUF, src, src + G::VIMG, DMA};
-    apply_zw<B, true>(Vs, Vs + G::VIMG, X, H, W, 0, d);
+    if constexpr (DMA) {
+      DmaJob<B> d{lds + (buf ^ 1) * BUF, src, src + G::VIMG};
+      apply_zw<B, true>(Vs, Vs + G::VIMG, X, H, W, 0, d);
+    } else {
+      apply_zw<B, true>(Vs, Vs + G::VIMG, X, H, W, 0);
+    }
     apply_x<B, true>(Vs, X, W, 0);
     buf ^= 1;
   }
