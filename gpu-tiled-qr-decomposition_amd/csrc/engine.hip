@@ -65,6 +65,8 @@ __device__ unsigned long long g_fst[4096 * 16];  // >= FST_N categories per work
 #include "flow.hpp"
 namespace tqr {
 static_assert(FST_N <= 16, "g_fst holds 16 categories per workgroup");
+static_assert(Geo<256>::TPIMG == 1024 && Geo<16>::TPIMG == 256, "host tpimg_doubles mirrors Geo::TPIMG");
+static_assert(Geo<256>::TPK <= Geo<256>::TSZ && Geo<16>::TPK <= Geo<16>::TSZ, "packed T fits the Gram buffer");
 
 template <int B>
 __device__ __forceinline__ double* tw_ptr(const Args& a, int i, int k, int g) {
@@ -523,10 +525,14 @@ static size_t vimg_doubles(int b) {
   const size_t ib = b < 32 ? b : 32;
   return ((size_t)b * (ib + 2) + 127) / 128 * 128;
 }
+static size_t tpimg_doubles(int b) {  // packed T image (Geo<b>::TPIMG)
+  const size_t nri = (b < 32 ? b : 32) / 4;
+  return (16 * nri * nri + 127) / 128 * 128;
+}
 // flow engine workspace of one step with `rows` tile rows (flow.hpp flow_vw_off / flow_tw_off)
 static size_t wk_bytes(int b, int rows) {
   const size_t ng = b / (b < 32 ? b : 32);
-  return (size_t)rows * ng * (vimg_doubles(b) + timg_doubles(b)) * sizeof(double);
+  return (size_t)rows * ng * (vimg_doubles(b) + tpimg_doubles(b)) * sizeof(double);
 }
 
 }  // namespace tqr

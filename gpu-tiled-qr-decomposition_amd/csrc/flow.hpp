@@ -155,7 +155,7 @@ __device__ __forceinline__ size_t flow_vw_off(int p, int i, int k, int g) {
 template <int B>
 __device__ __forceinline__ size_t flow_tw_off(int p, int i, int k, int g) {
   using G = Geo<B>;
-  return (size_t)(p - k) * G::NG * G::VIMG + ((size_t)(i - k) * G::NG + g) * G::TIMG;
+  return (size_t)(p - k) * G::NG * G::VIMG + ((size_t)(i - k) * G::NG + g) * G::TPIMG;
 }
 template <int B>
 __device__ __forceinline__ double* flow_tw(const FlowArgs& a, int i, int k, int g) {
@@ -178,7 +178,7 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 // (V image instructions first, then T), so the issue cost hides under the MFMA stream.
 template <int B>
 struct DmaJob {
-  static constexpr int NIV = Geo<B>::VIMG / 128, NIT = Geo<B>::TIMG / 128;
+  static constexpr int NIV = Geo<B>::VIMG / 128, NIT = Geo<B>::TPIMG / 128;
   static constexpr int PV = (NIV + FLOW_NW - 1) / FLOW_NW, PT = (NIT + FLOW_NW - 1) / FLOW_NW;
   static constexpr int STEPS = PV + PT;
   double* dst;
@@ -366,11 +366,15 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     }
     FST(10);
     build_t<B>(Vs, tauv, Gs, Ts, Gp, qrs ? ks0 : 0);
+    // packed T (the Gram buffer is free now): the trailing update's and the chains' T operand
+    double* Tp = Gs;
+    pack_t<B, FLOW_NT>(Ts, Tp);
+    __syncthreads();
     FST(11);
-    {  // V image (explicit) and T image of this group for the chains (LDS-DMA sources)
+    {  // V image (explicit) and packed T image of this group for the chains (LDS-DMA sources)
       double* tg = flow_tw<B>(a, qrs ? k : l, k, g);
       double* vg = flow_vw<B>(a, qrs ? k : l, k, g);
-      for (int idx = t; idx < G::TSZ; idx += FLOW_NT) st(tg + idx, Ts[idx]);
+      for (int idx = t; idx < G::TPIMG; idx += FLOW_NT) st(tg + idx, Tp[idx]);
       for (int idx = t; idx < G::VSZ; idx += FLOW_NT) st(vg + idx, Vs[vimg_row(idx / VP) * VP + idx % VP]);
     }
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
@@ -387,12 +391,12 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       const int col = c0 + IB + 16 * s;
       if (qrs) {
         load_strip<B, S, true>(X, Rt, ldm, col, ks0);
-        apply_group<B, false, FLOW_PF>(Vs, Ts, X, H, ks0);
+        apply_group<B, false, FLOW_PF, true>(Vs, Tp, X, H, ks0);
         store_strip<B>(X, Rt, ldm, col, ks0);
       } else {
         load_strip<B, S, true>(X, Bt, ldm, col, 0);
         load_head<B, S, true>(H, Rt, ldm, c0, col);
-        apply_group<B, true, FLOW_PF>(Vs, Ts, X, H, 0);
+        apply_group<B, true, FLOW_PF, true>(Vs, Tp, X, H, 0);
         store_strip<B>(X, Bt, ldm, col, 0);
         store_head<B>(H, Rt, ldm, c0, col);
       }
@@ -426,7 +430,7 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
       const __amdgpu_buffer_rsrc_t vdst = uniform_rsrc(pw + vo), tdst = uniform_rsrc(pw + to);
       for (int c = t; c < G::VIMG / 2; c += FLOW_NT)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(vsrc, 16 * c, 0, 16), vdst, 16 * c, 0, 17);
-      for (int c = t; c < G::TIMG / 2; c += FLOW_NT)
+      for (int c = t; c < G::TPIMG / 2; c += FLOW_NT)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(tsrc, 16 * c, 0, 16), tdst, 16 * c, 0, 17);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -456,7 +460,7 @@ template <int B, typename S>
 __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1, int j, int k, int seg, double* lds,
                                         int* sflag) {
   using G = Geo<B>;
-  constexpr int IB = G::IB, NG = G::NG, BUF = G::VIMG + G::TIMG;
+  constexpr int IB = G::IB, NG = G::NG, BUF = G::VIMG + G::TPIMG;
   S* A = (S*)a.A;
   const size_t ldm = a.ldm;
   const int t = threadIdx.x, w = t >> 6;
@@ -562,13 +566,13 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
 #endif
 #ifdef TQR_DIAG_NODMA  // what-if: no staging at all
       if (active) {
-        if (ts) apply_zw<B, true, NoHook, FLOW_PF>(Vs, Ts, X, H, W, 0);
-        else apply_zw<B, false, NoHook, FLOW_PF>(Vs, Ts, X, H, W, g * IB / 4);
+        if (ts) apply_zw<B, true, NoHook, FLOW_PF, true>(Vs, Ts, X, H, W, 0);
+        else apply_zw<B, false, NoHook, FLOW_PF, true>(Vs, Ts, X, H, W, g * IB / 4);
       }
 #else
       if (active) {
-        if (ts) apply_zw<B, true, DmaJob<B>, FLOW_PF>(Vs, Ts, X, H, W, 0, d);
-        else apply_zw<B, false, DmaJob<B>, FLOW_PF>(Vs, Ts, X, H, W, g * IB / 4, d);
+        if (ts) apply_zw<B, true, DmaJob<B>, FLOW_PF, true>(Vs, Ts, X, H, W, 0, d);
+        else apply_zw<B, false, DmaJob<B>, FLOW_PF, true>(Vs, Ts, X, H, W, g * IB / 4, d);
       } else {
         for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
       }
@@ -618,7 +622,7 @@ template <int B>
 constexpr int flow_lds_doubles() {
   using G = Geo<B>;
   constexpr int panel = G::VSZ + 8 * G::TSZ + G::IB + 2 + 2 * 4 * 32 + 4 * 32 + 2 * 32;
-  constexpr int chain = 2 * (G::VIMG + G::TIMG);
+  constexpr int chain = 2 * (G::VIMG + G::TPIMG);
   return panel > chain ? panel : chain;
 }
 

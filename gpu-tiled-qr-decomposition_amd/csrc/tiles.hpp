@@ -63,6 +63,9 @@ struct Geo {
   // workspace slots / LDS-DMA images, rounded up to whole KiB (128 doubles)
   static constexpr int VIMG = (VSZ + 127) / 128 * 128;
   static constexpr int TIMG = (TSZ + 127) / 128 * 128;
+  // packed T image (pack_t): lane-major blocks of -T, what apply_zw<..., TPACK=true> reads
+  static constexpr int TPK = 16 * NRI * NRI;
+  static constexpr int TPIMG = (TPK + 127) / 128 * 128;
   // V image column permutation: the NRI values a lane needs per row are contiguous.
   __device__ static constexpr int pc(int c) { return (c & 3) * NRI + (c >> 2); }
 };
@@ -116,7 +119,9 @@ struct NoHook {
 };
 // PF: software-pipelined LDS operand reads (needed at one wave per SIMD; at two waves per SIMD
 // the other wave hides the latency and the registers are better spent elsewhere)
-template <int B, bool HEAD, typename Hook = NoHook, bool PF = true>
+// TPACK: Ts is the packed image of pack_t (W = -T^T Z as NRI batches of independent MFMAs with
+// 16-B operand reads one batch ahead) instead of the row-major T (one 8-B read per MFMA).
+template <int B, bool HEAD, typename Hook = NoHook, bool PF = true, bool TPACK = false>
 __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const double* __restrict__ Ts,
                                          const double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI],
                                          double (&W)[Geo<B>::NRI], int ks0, const Hook& hook = Hook()) {
@@ -155,13 +160,38 @@ __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const do
     }
   }
   for (int m = NKS / 2; m < Hook::STEPS; ++m) hook.step(m);
-  // W = -T^T Z   (A operand: T[4k2+x][4wi+y]); T upper triangular -> k2 <= wi.
+  if constexpr (TPACK) {
+    // W = -T^T Z, k-block by k-block: batch kb is the NRI - kb independent MFMAs W[wi] +=
+    // (-T)[kb-block][wi-block]^T Z[kb], wi >= kb; its operands (the lane's NRI values of
+    // block row kb, contiguous in the packed image) are read while batch kb-1 runs.
+    auto ldt = [&](double (&a)[NRI], int kb) {
+      const double2* tr = reinterpret_cast<const double2*>(Ts + ((kb * 4 + x) * 4 + y) * NRI);
 #pragma unroll
-  for (int wi = 0; wi < NRI; ++wi) {
-    double acc = 0.0;
+      for (int h = 0; h < NRI / 2; ++h) {
+        const double2 v = tr[h];
+        a[2 * h] = v.x;
+        a[2 * h + 1] = v.y;
+      }
+    };
+    double tc[NRI], tn[NRI];
+    ldt(tc, 0);
 #pragma unroll
-    for (int k2 = 0; k2 <= wi; ++k2) acc = mfma4(Ts[(4 * k2 + x) * TP + 4 * wi + y], Z[k2], acc);
-    W[wi] = -acc;
+    for (int kb = 0; kb < NRI; ++kb) {
+      if (kb + 1 < NRI) ldt(tn, kb + 1);
+#pragma unroll
+      for (int wi = kb; wi < NRI; ++wi) W[wi] = mfma4(tc[wi], Z[kb], kb == 0 ? 0.0 : W[wi]);
+#pragma unroll
+      for (int r = 0; r < NRI; ++r) tc[r] = tn[r];
+    }
+  } else {
+    // W = -T^T Z   (A operand: T[4k2+x][4wi+y]); T upper triangular -> k2 <= wi.
+#pragma unroll
+    for (int wi = 0; wi < NRI; ++wi) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k2 = 0; k2 <= wi; ++k2) acc = mfma4(Ts[(4 * k2 + x) * TP + 4 * wi + y], Z[k2], acc);
+      W[wi] = -acc;
+    }
   }
   if (HEAD) {
 #pragma unroll
@@ -216,11 +246,11 @@ __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&
   }
 }
 
-template <int B, bool HEAD, bool PF = true>
+template <int B, bool HEAD, bool PF = true, bool TPACK = false>
 __device__ __forceinline__ void apply_group(const double* __restrict__ Vs, const double* __restrict__ Ts,
                                             double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI], int ks0) {
   double W[Geo<B>::NRI];
-  apply_zw<B, HEAD, NoHook, PF>(Vs, Ts, X, H, W, ks0);
+  apply_zw<B, HEAD, NoHook, PF, TPACK>(Vs, Ts, X, H, W, ks0);
   apply_x<B, HEAD, PF>(Vs, X, W, ks0);
 }
 
@@ -350,6 +380,18 @@ template <int B>
 __device__ __forceinline__ void stage_t(double* Ts, const double* __restrict__ tg) {
   using g = Geo<B>;
   for (int idx = threadIdx.x; idx < g::IB * g::TP; idx += NT) Ts[idx] = tg[idx];
+}
+
+// Packed T image: Tp[((kb * 4 + x) * 4 + y) * NRI + wi] = -T[4kb + x][4wi + y] (0 for wi < kb),
+// i.e. the A operands of W = -T^T Z for lane (x, y) and k-block kb, contiguous over wi.
+template <int B, int NTH>
+__device__ __forceinline__ void pack_t(const double* Ts, double* Tp) {
+  using g = Geo<B>;
+  constexpr int NRI = g::NRI;
+  for (int idx = threadIdx.x; idx < g::TPIMG; idx += NTH) {
+    const int wi = idx % NRI, y = (idx / NRI) & 3, x = (idx / (4 * NRI)) & 3, kb = idx / (16 * NRI);
+    Tp[idx] = idx < g::TPK && kb <= wi ? -Ts[(4 * kb + x) * g::TP + 4 * wi + y] : 0.0;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
