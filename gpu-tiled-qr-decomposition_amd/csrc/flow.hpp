@@ -207,10 +207,7 @@ struct DmaJob {
   // over-waits when it does not see these (in-order counter), never under-waits.
   static __device__ __forceinline__ void dma16(const double* src, double* lds_wave) {
     const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void_t*)lds_wave);
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(src), "s"(l) : "memory", "m0");
-#pragma clang diagnostic pop
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(src), "{m0}"(l) : "memory");
   }
 };
 
@@ -493,7 +490,6 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
   const int ifirst = seg == 0 ? k : i0;
   for (int i = ifirst; i < i1 || i == k; i = (i == k ? i0 : i + 1)) {
     const bool ts = i != k;
-    const int need = i - k + 1;  // members of panel k that must have finished a group
     {
       bool ok = true;
       if (t == 0) {
@@ -518,15 +514,20 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
     }
     dma_next = false;
     // head rows: written by another workgroup before this segment or by this one (sc1 loads
-    // for both: one code path, no branch in the MFMA stream)
-    if (FLOW_PF && ts && active) load_head<B, S, true>(H, At, ldm, 0, col);
+    // for both). The UNMQR element (i == k, GE-type V) runs the very same TSMQR code with a zero
+    // head: its V image is explicit (zeros above the unit diagonal), so Z = 0 + V^T X and X += V W
+    // are exactly the GE update (the zero rows add exact zeros) — one MFMA stream for both
+    // element types keeps the register allocation of the hot TSMQR path clean (a separate GE
+    // variant with ks0-skipping cost the TSMQR phase 2 its operand prefetch), for ~1 % extra flops.
+    const __amdgpu_buffer_rsrc_t hrs = head_rsrc(At, ts);  // UNMQR: empty resource, head = 0
+    const unsigned hoff = head_off<B, S>(ldm, 0, col);
+    if (FLOW_PF && active) load_head_buf<B, S, 16>(H, hrs, hoff);
     FST(4);
     const int inext = (i == k) ? i0 : i + 1;
     const bool has_next = inext < i1;
-    // the group loop, unswitched on the element type (TSMQR / UNMQR) so that each copy is one
-    // straight MFMA stream with no per-group branches on the type
-    auto groups = [&](auto ts_c) -> bool {
-    constexpr bool ts = decltype(ts_c)::value;
+    // the group loop as a lambda with a single exit (an early return out of the loop itself made
+    // the register allocator spill ~1 KiB around the poll calls)
+    auto groups = [&]() -> bool {
     for (int g = 0; g < NG; ++g) {
       {
         bool ok = true;
@@ -551,7 +552,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
         if (g + 1 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
       }
       FST(7);
-      if (!FLOW_PF && ts && active) load_head<B, S, true>(H, At, ldm, g * IB, col);  // 2 waves/SIMD
+      if (!FLOW_PF && active) load_head_buf<B, S, 16>(H, hrs, hoff + g * IB * sizeof(S));  // 2 waves/SIMD
       const double* Vs = lds + buf * BUF;
       const double* Ts = Vs + G::VIMG;
       // the other buffer is free (every wave passed this sync point): next DMA rides phase 1
@@ -565,34 +566,23 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
       d.t = flow_tw<B>(a, k, k, 0);
 #endif
 #ifdef TQR_DIAG_NODMA  // what-if: no staging at all
-      if (active) {
-        if (ts) apply_zw<B, true, NoHook, FLOW_PF, true>(Vs, Ts, X, H, W, 0);
-        else apply_zw<B, false, NoHook, FLOW_PF, true>(Vs, Ts, X, H, W, g * IB / 4);
-      }
+      if (active) apply_zw<B, true, NoHook, FLOW_PF, true>(Vs, Ts, X, H, W, 0);
 #else
-      if (active) {
-        if (ts) apply_zw<B, true, DmaJob<B>, FLOW_PF, true>(Vs, Ts, X, H, W, 0, d);
-        else apply_zw<B, false, DmaJob<B>, FLOW_PF, true>(Vs, Ts, X, H, W, g * IB / 4, d);
-      } else {
+      if (active) apply_zw<B, true, DmaJob<B>, FLOW_PF, true>(Vs, Ts, X, H, W, 0, d);
+      else
         for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
-      }
 #endif
       FST(3);
-#ifdef TQR_DIAG_NOHEAD
-      if (false) {
-#else
-      if (ts && active) {
-#endif
+#ifndef TQR_DIAG_NOHEAD
+      if (active) {
         // head rows stay with this workgroup for the whole segment: plain (write-back) stores,
         // made visible to the next segment's workgroup by one release before the Ac publish
-        store_head_plain<B>(H, At, ldm, g * IB, col);
-        if (FLOW_PF && g + 1 < NG) load_head<B, S, true>(Hn, At, ldm, (g + 1) * IB, col);
+        store_head_buf<B, S, 0>(H, hrs, hoff + g * IB * sizeof(S));
+        if (FLOW_PF && g + 1 < NG) load_head_buf<B, S, 16>(Hn, hrs, hoff + (g + 1) * IB * sizeof(S));
       }
+#endif
       FST(2);
-      if (active) {
-        if (ts) apply_x<B, true, FLOW_PF>(Vs, X, W, 0);
-        else apply_x<B, false, FLOW_PF>(Vs, X, W, g * IB / 4);
-      }
+      if (active) apply_x<B, true, FLOW_PF>(Vs, X, W, 0);
       FST(3);
       if (FLOW_PF) {
 #pragma unroll
@@ -602,7 +592,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
     }
     return true;
     };
-    if (!(ts ? groups(std::true_type{}) : groups(std::false_type{}))) return;
+    if (!groups()) return;
 #ifndef TQR_DIAG_NOSTRIP
     if (active) store_strip_pair<B, S>(X, Xt, ldm, col);
 #endif

@@ -301,15 +301,17 @@ __device__ __forceinline__ void load_strip_pair(double (&X)[Geo<B>::NKS], S* til
   const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
   __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile);
   const unsigned base = (unsigned)(((size_t)c * ldm + 2 * x) * sizeof(S));
+  // per-access displacement in the scalar offset (one VGPR offset for the whole strip: an
+  // unsigned voffset + constant cannot be folded into the immediate field without a no-wrap proof)
 #pragma unroll
   for (int h = 0; h < Geo<B>::NKS / 2; ++h) {
-    const unsigned off = base + 8 * h * sizeof(S);
+    const int so = 8 * h * sizeof(S);
     if constexpr (sizeof(S) == 8) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, base, so, 16);
       X[2 * h] = __longlong_as_double(((long long)v[1] << 32) | v[0]);
       X[2 * h + 1] = __longlong_as_double(((long long)v[3] << 32) | v[2]);
     } else {
-      auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 16);
+      auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, base, so, 16);
       X[2 * h] = (double)__uint_as_float(v[0]);
       X[2 * h + 1] = (double)__uint_as_float(v[1]);
     }
@@ -322,15 +324,56 @@ __device__ __forceinline__ void store_strip_pair(const double (&X)[Geo<B>::NKS],
   const unsigned base = (unsigned)(((size_t)c * ldm + 2 * x) * sizeof(S));
 #pragma unroll
   for (int h = 0; h < Geo<B>::NKS / 2; ++h) {
-    const unsigned off = base + 8 * h * sizeof(S);
+    const int so = 8 * h * sizeof(S);
     if constexpr (sizeof(S) == 8) {
       const unsigned long long a = (unsigned long long)__double_as_longlong(X[2 * h]);
       const unsigned long long b = (unsigned long long)__double_as_longlong(X[2 * h + 1]);
       __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
-      __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, base, so, 16);
     } else {
       __attribute__((ext_vector_type(2))) unsigned v = {__float_as_uint((float)X[2 * h]), __float_as_uint((float)X[2 * h + 1])};
-      __builtin_amdgcn_raw_buffer_store_b64(v, rs, off, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b64(v, rs, base, so, 16);
+    }
+  }
+}
+// Head rows through a buffer resource (chain engine): base = byte offset of (row r0 + x,
+// column col0 + 4blk + y); soffset carries 4 rows per access. A resource with num_records = 0
+// makes every load return 0 and drops every store — the branch-free "no head" of the UNMQR
+// element (flow_chain).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const void* p, bool on) {
+  const unsigned long long u = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  const int n = __builtin_amdgcn_readfirstlane(on ? 0x7fffffff : 0);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, n, 0x00020000);
+}
+template <int B, typename S>
+__device__ __forceinline__ unsigned head_off(size_t ldm, int r0, int col0) {
+  const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
+  return (unsigned)(((size_t)c * ldm + r0 + x) * sizeof(S));
+}
+template <int B, typename S, int AUX>
+__device__ __forceinline__ void load_head_buf(double (&H)[Geo<B>::NRI], __amdgpu_buffer_rsrc_t rs, unsigned base) {
+#pragma unroll
+  for (int r = 0; r < Geo<B>::NRI; ++r) {
+    if constexpr (sizeof(S) == 8) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, base, 4 * r * 8, AUX);
+      H[r] = __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
+    } else {
+      H[r] = (double)__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, base, 4 * r * 4, AUX));
+    }
+  }
+}
+template <int B, typename S, int AUX>
+__device__ __forceinline__ void store_head_buf(const double (&H)[Geo<B>::NRI], __amdgpu_buffer_rsrc_t rs, unsigned base) {
+#pragma unroll
+  for (int r = 0; r < Geo<B>::NRI; ++r) {
+    if constexpr (sizeof(S) == 8) {
+      const unsigned long long u = (unsigned long long)__double_as_longlong(H[r]);
+      __attribute__((ext_vector_type(2))) unsigned v = {(unsigned)u, (unsigned)(u >> 32)};
+      __builtin_amdgcn_raw_buffer_store_b64(v, rs, base, 4 * r * 8, AUX);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)H[r]), rs, base, 4 * r * 4, AUX);
     }
   }
 }
