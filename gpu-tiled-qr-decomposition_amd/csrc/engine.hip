@@ -853,6 +853,8 @@ int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, in
   return TQR_OK;
 }
 
+int tqr_flow_strip_width(void) { return FLOW_SW; }
+
 int tqr_flow_plan_check(int M, int N, int b, int seglen, int* ntasks, int* est_order) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1) return TQR_EINVAL;
   FlowPlan fp;

@@ -40,8 +40,10 @@ constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel memb
 // 1 panel waits, 2 chain head-row I/O, 3 chain apply (with the LDS-DMA issue), 4 chain strip
 // I/O + publish, 5 panel compute, 6 dequeue/dispatch + kernel exit, 7 chain drain + barrier,
 // 8 chain Tc waits (tile's previous step), 9 chain Ac waits (previous segment), 10 panel I/O +
-// writeback + images, 11 panel build_t, 12 panel in-tile trailing update (+ its Rt publish).
-constexpr int FST_N = 13;
+// writeback + images, 11 panel build_t, 12 panel in-tile trailing update (+ its Rt publish),
+// 13 chain phase 2 (X += V W; 3 is then phase 1 Z alone), 14 chain next-head load, 15 chain
+// W = -T^T Z + head update.
+constexpr int FST_N = 16;
 #ifdef TQR_FLOW_STAMPS
 extern __device__ unsigned long long g_fst[];
 #define FST(c)                                                                            \
@@ -56,12 +58,14 @@ extern __device__ unsigned long long g_fst[];
 #else
 #define FST(c) do {} while (0)
 #endif
-// 256 threads = 4 waves = one wave per SIMD (the register budget of the chain: X strip 128 VGPRs,
-// operands and prefetches in the accumulator file). An 8-wave / 128-column-strip variant
-// (FLOW_NT = 512: half the LDS-DMA bytes per flop, two waves per SIMD, apply_zw/apply_x without
-// read pipelining — 64.8 TF/s in tools/ubench/apply_bench.hip) compiles, but the chain then
-// exceeds the 256-register budget of two waves per SIMD and spills inside the MFMA loops.
-constexpr int FLOW_NT = 256;
+// 512 threads = 8 waves = two waves per SIMD: a chain task updates a 128-column strip, so each
+// LDS-DMA'd V/T image serves twice the flops of the 4-wave / 64-column form, and each SIMD's
+// second wave issues MFMAs while the first waits on LDS, the memory pipeline or a barrier.
+// The register budget is then 256 per wave (X strip 128, operands unpipelined — FLOW_PF off);
+// it fits without inner-loop spills once the counter polls are global (not FLAT) loads and the
+// UNMQR element shares the TSMQR code (see flow_chain). 4 waves (FLOW_NT = 256, pipelined operand
+// reads) measured 159 ms at 16384^2 against 148.5 ms for this form.
+constexpr int FLOW_NT = 512;
 constexpr int FLOW_NW = FLOW_NT / 64;      // waves
 constexpr int FLOW_SW = 16 * FLOW_NW;      // strip width (columns) of a chain task
 constexpr bool FLOW_PF = FLOW_NW <= 4;     // software-pipelined operand reads (1 wave/SIMD)
@@ -99,10 +103,29 @@ struct FlowArgs {
 };
 
 // ---- synchronisation ---------------------------------------------------------------------
-__device__ __forceinline__ int ld_relaxed(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// Counter accesses go through global (address-space 1) pointers: a generic pointer makes them
+// FLAT instructions, which also count on the LDS counter (lgkmcnt) and return out of order with
+// LDS reads — one such poll in flight turned every operand wait of the MFMA stream that
+// followed into lgkmcnt(0).
+typedef __attribute__((address_space(1))) int gint;
+__device__ __forceinline__ gint* gptr(int* p) { return (gint*)p; }
+__device__ __forceinline__ int ld_relaxed(int* p) {
+  return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-__device__ __forceinline__ int ld_sys(int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
+__device__ __forceinline__ int ld_sys(int* p) { return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }
 __device__ __forceinline__ int ld_cnt(int* p, bool sys) { return sys ? ld_sys(p) : ld_relaxed(p); }
+
+// Wave-uniform copies (SGPRs): arguments of a device function arrive in VGPRs, and without a
+// readfirstlane the compiler keeps every value derived from them per lane.
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+template <typename T>
+__device__ __forceinline__ T* uni(T* p) {
+  const unsigned long long u = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return (T*)(((unsigned long long)hi << 32) | lo);
+}
 
 // thread 0 only: spin until *p >= target; false on error / timeout. sys: the counter is written
 // by other devices (system-scope polls)
@@ -142,8 +165,8 @@ __device__ __forceinline__ void wg_publish(int* p, int delta, bool sys = false) 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (sys) __hip_atomic_fetch_add(p, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    else __hip_atomic_fetch_add(p, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sys) __hip_atomic_fetch_add(gptr(p), delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_fetch_add(gptr(p), delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -184,6 +207,8 @@ struct DmaJob {
   double* dst;
   const double* v;
   const double* t;
+  int* sflag;  // activity stamps only
+  __device__ __forceinline__ void mid() const { FST(3); }
   // Branch-free: every wave issues exactly STEPS instructions (a wave past the end of an image
   // re-copies its last KiB — identical bytes to the same LDS words), and a job with nothing to
   // fetch is pointed by the caller at an image it may legally re-read into the idle buffer.
@@ -228,7 +253,7 @@ __device__ __forceinline__ bool sync_point(bool ok0, int* sflag, int& par) {
 }
 // thread 0, after a draining sync point (every wave's sc1 stores complete): bump a counter
 __device__ __forceinline__ void publish_after_drain(int* p, int delta) {
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(p, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(gptr(p), delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Thread 0's view of one panel's group counters Rc[k][0..NG): rv[g] (LDS, thread 0 only) holds
@@ -454,8 +479,9 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
 // The tile-strip counter Tc of an element is published after the next element's first drain
 // (its stores are complete by then), so no wave waits for its own stores to land.
 template <int B, typename S>
-__device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1, int j, int k, int seg, double* lds,
-                                        int* sflag) {
+__device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int i1_, int j_, int k_, int seg_,
+                                        double* lds, int* sflag) {
+  const int s = uni(s_), i0 = uni(i0_), i1 = uni(i1_), j = uni(j_), k = uni(k_), seg = uni(seg_);
   using G = Geo<B>;
   constexpr int IB = G::IB, NG = G::NG, BUF = G::VIMG + G::TPIMG;
   S* A = (S*)a.A;
@@ -464,9 +490,18 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
   const int col = s * FLOW_SW + 16 * w;  // this wave's 16 columns inside the tile
   const bool active = B % FLOW_SW == 0 || col < B;  // (compile-time true unless B < FLOW_SW)
   S* At = A + (size_t)j * B * ldm + (size_t)k * B;  // tile (k,j): the chain's head rows
+  // everything the group loop needs from FlowArgs, read once per task: the asm memory clobbers
+  // of the sync points would otherwise force a reload per group — for Wk[k] a global load whose
+  // latency sat in front of the group's first LDS-DMA
+  double* const wk = uni(a.Wk[k]);
+  const int P = uni(a.p), Q = uni(a.q), NS = uni(a.ns);
+  int* const err = uni(a.err);
+  int* const Tc = uni(a.Tc);
+  auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B>(P, i_, k, g_); };
+  auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B>(P, i_, k, g_); };
   int* const rc = &a.Rc[(size_t)k * NG];
-  int* const ac = &a.Ac[((size_t)k * a.q + j) * a.ns + s];
-  auto tc = [&](int i) { return &a.Tc[((size_t)i * a.q + j) * a.ns + s]; };
+  int* const ac = &a.Ac[((size_t)k * Q + j) * NS + s];
+  auto tc = [&](int i) { return &Tc[((size_t)i * Q + j) * NS + s]; };
   double X[G::NKS];
   double H[G::NRI], Hn[G::NRI], W[G::NRI];
   int buf = 0, par = 0;
@@ -477,14 +512,14 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
   int tc_pf = -1;  // thread 0: Tc of the next element's tile, loaded one group ahead
   // multi-GPU, panel owned by another rank: per-member flags forwarded by the owner
   const bool remote = a.dist && (k % a.world != a.rank);
-  int* const rf = a.Rf + (size_t)k * a.p * NG;
+  int* const rf = a.Rf + (size_t)k * P * NG;
   int* fl_pf = nullptr;  // thread 0: the flag the next sync point tests, and its early load
   int fl_pv = 0;
   auto ready = [&](int i_, int g_) -> bool {
-    if (!remote) return pv.ensure(rc, g_, i_ - k + 1, a.err, false);
+    if (!remote) return pv.ensure(rc, g_, i_ - k + 1, err, false);
     int* fp = rf + (size_t)i_ * NG + g_;
     if (fp == fl_pf && fl_pv >= 1) return true;
-    return spin_ge(fp, 1, a.err, true);
+    return spin_ge(fp, 1, err, true);
   };
   FST(6);
   const int ifirst = seg == 0 ? k : i0;
@@ -493,9 +528,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
     {
       bool ok = true;
       if (t == 0) {
-        if (i == ifirst && seg > 0) ok = spin_ge(ac, seg, a.err);
+        if (i == ifirst && seg > 0) ok = spin_ge(ac, seg, err);
         FST(9);
-        if (ok && k > 0 && tc_pf < k) ok = spin_ge(tc(i), k, a.err);
+        if (ok && k > 0 && tc_pf < k) ok = spin_ge(tc(i), k, err);
         tc_pf = -1;
         FST(8);
         if (ok && !dma_next) ok = ready(i, 0);
@@ -509,7 +544,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
     if (active) load_strip_pair<B, S>(X, Xt, ldm, col);
 #endif
     if (!dma_next) {
-      DmaJob<B> d{lds + buf * BUF, flow_vw<B>(a, i, k, 0), flow_tw<B>(a, i, k, 0)};
+      DmaJob<B> d{lds + buf * BUF, vimg(i, 0), timg(i, 0), sflag};
       for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
     }
     dma_next = false;
@@ -559,11 +594,11 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
       // (nothing next: re-read this group's own images into the idle buffer, keeping the
       // DMA stream branch-free)
       const int gd = g + 1 < NG ? g + 1 : has_next ? 0 : g, id = g + 1 < NG ? i : has_next ? inext : i;
-      DmaJob<B> d{lds + (buf ^ 1) * BUF, flow_vw<B>(a, id, k, gd), flow_tw<B>(a, id, k, gd)};
+      DmaJob<B> d{lds + (buf ^ 1) * BUF, vimg(id, gd), timg(id, gd), sflag};
       dma_next = g + 1 == NG && has_next;
 #if defined(TQR_DIAG_DMA_FIXED)  // what-if: every DMA reads one L2-hot image
-      d.v = flow_vw<B>(a, k, k, 0);
-      d.t = flow_tw<B>(a, k, k, 0);
+      d.v = vimg(k, 0);
+      d.t = timg(k, 0);
 #endif
 #ifdef TQR_DIAG_NODMA  // what-if: no staging at all
       if (active) apply_zw<B, true, NoHook, FLOW_PF, true>(Vs, Ts, X, H, W, 0);
@@ -572,18 +607,19 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s, int i0, int i1
       else
         for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
 #endif
-      FST(3);
+      FST(15);
 #ifndef TQR_DIAG_NOHEAD
       if (active) {
         // head rows stay with this workgroup for the whole segment: plain (write-back) stores,
         // made visible to the next segment's workgroup by one release before the Ac publish
         store_head_buf<B, S, 0>(H, hrs, hoff + g * IB * sizeof(S));
+        FST(2);
         if (FLOW_PF && g + 1 < NG) load_head_buf<B, S, 16>(Hn, hrs, hoff + (g + 1) * IB * sizeof(S));
       }
 #endif
-      FST(2);
+      FST(14);
       if (active) apply_x<B, true, FLOW_PF>(Vs, X, W, 0);
-      FST(3);
+      FST(13);
       if (FLOW_PF) {
 #pragma unroll
         for (int r = 0; r < G::NRI; ++r) H[r] = Hn[r];

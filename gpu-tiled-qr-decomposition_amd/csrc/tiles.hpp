@@ -115,6 +115,7 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 // next group's LDS-DMA there (flow.hpp), so its issue cost hides under the MFMAs.
 struct NoHook {
   __device__ __forceinline__ void step(int) const {}
+  __device__ __forceinline__ void mid() const {}  // between Z and W (activity stamps)
   static constexpr int STEPS = 0;
 };
 // PF: software-pipelined LDS operand reads (needed at one wave per SIMD; at two waves per SIMD
@@ -147,7 +148,11 @@ __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const do
   if (PF) ldz(ac, HEAD ? 0 : ks0);
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
-    asm volatile("" ::: "memory");  // one k-step per region: bounds the hoisting of LDS reads
+    // one k-step per scheduling region: the memory clobber bounds the LDS reads, the
+    // sched_barrier the MFMAs (left free, the scheduler pulls the next k-step's MFMAs up against
+    // their just-issued operand reads and every wait becomes lgkmcnt(0))
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
     if ((ks & 1) == 0) hook.step(ks / 2);
     if (!HEAD && ks < ks0) continue;
     if (!PF) ldz(ac, ks);
@@ -160,6 +165,7 @@ __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const do
     }
   }
   for (int m = NKS / 2; m < Hook::STEPS; ++m) hook.step(m);
+  hook.mid();
   if constexpr (TPACK) {
     // W = -T^T Z, k-block by k-block: batch kb is the NRI - kb independent MFMAs W[wi] +=
     // (-T)[kb-block][wi-block]^T Z[kb], wi >= kb; its operands (the lane's NRI values of
@@ -177,6 +183,7 @@ __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const do
     ldt(tc, 0);
 #pragma unroll
     for (int kb = 0; kb < NRI; ++kb) {
+      __builtin_amdgcn_sched_barrier(0);
       if (kb + 1 < NRI) ldt(tn, kb + 1);
 #pragma unroll
       for (int wi = kb; wi < NRI; ++wi) W[wi] = mfma4(tc[wi], Z[kb], kb == 0 ? 0.0 : W[wi]);
@@ -199,9 +206,9 @@ __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const do
   }
 }
 
-template <int B, bool HEAD, bool PF = true>
+template <int B, bool HEAD, bool PF = true, typename Hook = NoHook>
 __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&X)[Geo<B>::NKS],
-                                        const double (&W)[Geo<B>::NRI], int ks0) {
+                                        const double (&W)[Geo<B>::NRI], int ks0, const Hook& hook = Hook()) {
   using g = Geo<B>;
   constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP;
   const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
@@ -223,7 +230,9 @@ __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&
   }
 #pragma unroll
   for (int kb = 0; kb < NKS; kb += 2) {
+    __builtin_amdgcn_sched_barrier(0);  // (see apply_zw)
     asm volatile("" ::: "memory");
+    hook.step(kb / 2);
     if (!HEAD && kb + 1 < ks0) continue;
     if (!PF) {
       ldx(bc[0], kb);
@@ -244,6 +253,7 @@ __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&
         for (int r = 0; r < NRI; ++r) bc[u][r] = bn[u][r];
     }
   }
+  for (int m = NKS / 2; m < Hook::STEPS; ++m) hook.step(m);
 }
 
 template <int B, bool HEAD, bool PF = true, bool TPACK = false>

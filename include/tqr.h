@@ -61,6 +61,9 @@ int tqr_plan_info(const tqr_plan* plan, int* engine, int* ntasks, int* est_order
 /* Host-only check of the persistent engine's task list for an M x N tile grid (no GPU):
  * number of tasks and whether the estimated-start-time order is topological. */
 int tqr_flow_plan_check(int M, int N, int b, int seglen, int* ntasks, int* est_order);
+/* Columns of one chain strip of the persistent engine (a tile column is split into
+ * ceil(b / width) strips; one workgroup updates one strip). */
+int tqr_flow_strip_width(void);
 
 /* Per-launch statistics of the last execute (filled when the plan was created with
  * tqr_plan_set_profile(plan, 1)): number of kernel launches and the summed device time of

@@ -83,7 +83,9 @@ def test_flow_plan_topological(tqr, M, N, b, seg):
     n, o = ctypes.c_int(), ctypes.c_int()
     assert tqr.lib().tqr_flow_plan_check(M, N, b, seg, ctypes.byref(n), ctypes.byref(o)) == 0
     kmax = min(M, N)
-    ns = (b + 63) // 64
+    sw = tqr.lib().tqr_flow_strip_width()
+    assert sw in (64, 128)
+    ns = (b + sw - 1) // sw
     panels = sum(M - k for k in range(kmax))
     chains = sum((N - k - 1) * ns * max(1, -(-(M - k - 1) // seg)) for k in range(kmax))
     assert n.value == panels + chains
