@@ -68,7 +68,7 @@ extern __device__ unsigned long long g_fst[];
 constexpr int FLOW_NT = 512;
 constexpr int FLOW_NW = FLOW_NT / 64;      // waves
 constexpr int FLOW_SW = 16 * FLOW_NW;      // strip width (columns) of a chain task
-constexpr bool FLOW_PF = FLOW_NW <= 4;     // software-pipelined operand reads (1 wave/SIMD)
+constexpr bool FLOW_PF = true;  // software-pipelined operand reads (also at 2 waves/SIMD)
 constexpr unsigned long long FLOW_TIMEOUT = 500000000ull;  // 5 s of s_memrealtime (100 MHz)
 
 // Multi-GPU (tile-column cyclic partition, one process per GPU): peer buffers opened by IPC.
