@@ -647,6 +647,15 @@ __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, 
   double* hrow = wb + 4 * 32;        // 2 x [32] GE head row broadcast (double-buffered)
   double* hout = hrow + 2 * 32;      // [IB][TP] TS updated head rows
   const int t = threadIdx.x;
+  if (t >= 256) {
+    // waves beyond the 4 row waves (8-wave engine): no rows, but they would still run the whole
+    // VALU reduction stream on zeros and compete with the row waves on their SIMDs — only
+    // match the row waves' barriers (one per reflector step, then the exit ones)
+    for (int C = 0; C < IB; ++C) __syncthreads();
+    __syncthreads();
+    if (TS) __syncthreads();
+    return;
+  }
   const bool own = t < B && (TS || t >= c0);
   double x[IB];
 #pragma unroll
@@ -661,7 +670,7 @@ __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, 
   }
   __syncthreads();
   if (TS) {
-    for (int idx = t; idx < IB * IB; idx += blockDim.x) {
+    for (int idx = t; idx < IB * IB; idx += 256) {
       const int r = idx / IB, c = idx % IB;
       if (r <= c) Hs[r * TP + c] = hout[r * TP + c];
     }
