@@ -59,12 +59,12 @@ __device__ unsigned long long g_pstamps[8];
 #endif
 
 #ifdef TQR_FLOW_STAMPS
-__device__ unsigned long long g_fst[4096 * 16];  // >= FST_N categories per workgroup
+__device__ unsigned long long g_fst[4096 * 24];  // >= FST_N categories per workgroup
 #endif
 }  // namespace tqr
 #include "flow.hpp"
 namespace tqr {
-static_assert(FST_N <= 16, "g_fst holds 16 categories per workgroup");
+static_assert(FST_N <= 24, "g_fst holds 24 categories per workgroup");
 static_assert(Geo<256>::TPIMG == 1024 && Geo<16>::TPIMG == 256, "host tpimg_doubles mirrors Geo::TPIMG");
 static_assert(Geo<256>::TPK <= Geo<256>::TSZ && Geo<16>::TPK <= Geo<16>::TSZ, "packed T fits the Gram buffer");
 

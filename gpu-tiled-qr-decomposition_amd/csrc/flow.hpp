@@ -42,8 +42,9 @@ constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel memb
 // 8 chain Tc waits (tile's previous step), 9 chain Ac waits (previous segment), 10 panel I/O +
 // writeback + images, 11 panel build_t, 12 panel in-tile trailing update (+ its Rt publish),
 // 13 chain phase 2 (X += V W; 3 is then phase 1 Z alone), 14 chain next-head load, 15 chain
-// W = -T^T Z + head update.
-constexpr int FST_N = 16;
+// W = -T^T Z + head update, 16 panel trailing: strip/head loads, 17 panel trailing: stores
+// (12 is then the trailing's MFMA part + Rt publish).
+constexpr int FST_N = 18;
 #ifdef TQR_FLOW_STAMPS
 extern __device__ unsigned long long g_fst[];
 #define FST(c)                                                                            \
@@ -344,13 +345,13 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
 #pragma unroll 8
       for (int idx = t; idx < B * IB; idx += FLOW_NT) {
         const int r = idx % B, c = idx / B;
-        Vs[r * VP + G::pc(c)] = r >= c0 ? ldc(Rt + (size_t)(c0 + c) * ldm + r) : 0.0;
+        Vs[vimg_inv(r) * VP + G::pc(c)] = r >= c0 ? ldc(Rt + (size_t)(c0 + c) * ldm + r) : 0.0;
       }
     } else {
 #pragma unroll 8
       for (int idx = t; idx < B * IB; idx += FLOW_NT) {
         const int r = idx % B, c = idx / B;
-        Vs[r * VP + G::pc(c)] = ldc(Bt + (size_t)(c0 + c) * ldm + r);
+        Vs[vimg_inv(r) * VP + G::pc(c)] = ldc(Bt + (size_t)(c0 + c) * ldm + r);
       }
       for (int idx = t; idx < IB * IB; idx += FLOW_NT) {
         const int r = idx % IB, c = idx / IB;
@@ -359,18 +360,20 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     }
     __syncthreads();
     FST(10);
-    if (qrs) panel_factor<B, false>(Vs, Hs, tauv, scratch, c0);
-    else panel_factor<B, true>(Vs, Hs, tauv, scratch, c0);
+    // Vs holds the panel rows in the chains' paired order (LDS row q = tile row vimg_row(q)): the
+    // V image is then a verbatim copy and the trailing update moves 16-B row pairs
+    if (qrs) panel_factor<B, false, true>(Vs, Hs, tauv, scratch, c0);
+    else panel_factor<B, true, true>(Vs, Hs, tauv, scratch, c0);
     FST(5);
     if (qrs) {
       for (int idx = t; idx < B * IB; idx += FLOW_NT) {
         const int r = idx % B, c = idx / B;
-        if (r >= c0) st(Rt + (size_t)(c0 + c) * ldm + r, Vs[r * VP + G::pc(c)]);
+        if (r >= c0) st(Rt + (size_t)(c0 + c) * ldm + r, Vs[vimg_inv(r) * VP + G::pc(c)]);
       }
     } else {
       for (int idx = t; idx < B * IB; idx += FLOW_NT) {
         const int r = idx % B, c = idx / B;
-        st(Bt + (size_t)(c0 + c) * ldm + r, Vs[r * VP + G::pc(c)]);
+        st(Bt + (size_t)(c0 + c) * ldm + r, Vs[vimg_inv(r) * VP + G::pc(c)]);
       }
       for (int idx = t; idx < IB * IB; idx += FLOW_NT) {
         const int r = idx % IB, c = idx / IB;
@@ -382,12 +385,12 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     if (qrs) {
       for (int idx = t; idx < B * IB; idx += FLOW_NT) {
         const int r = idx % B, c = idx / B, d = c0 + c;
-        if (r <= d) Vs[r * VP + G::pc(c)] = r == d ? 1.0 : 0.0;
+        if (r <= d) Vs[vimg_inv(r) * VP + G::pc(c)] = r == d ? 1.0 : 0.0;
       }
       __syncthreads();
     }
     FST(10);
-    build_t<B>(Vs, tauv, Gs, Ts, Gp, qrs ? ks0 : 0);
+    build_t<B>(Vs, tauv, Gs, Ts, Gp, 0);  // (permuted rows: the GE zero rows are not a prefix)
     // packed T (the Gram buffer is free now): the trailing update's and the chains' T operand
     double* Tp = Gs;
     pack_t<B, FLOW_NT>(Ts, Tp);
@@ -397,7 +400,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       double* tg = flow_tw<B>(a, qrs ? k : l, k, g);
       double* vg = flow_vw<B>(a, qrs ? k : l, k, g);
       for (int idx = t; idx < G::TPIMG; idx += FLOW_NT) st(tg + idx, Tp[idx]);
-      for (int idx = t; idx < G::VSZ; idx += FLOW_NT) st(vg + idx, Vs[vimg_row(idx / VP) * VP + idx % VP]);
+      for (int idx = t; idx < G::VSZ; idx += FLOW_NT) st(vg + idx, Vs[idx]);
     }
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
     wg_publish(&a.Rc[(size_t)k * NG + g], 1);
@@ -408,20 +411,29 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       FST(1);
     }
     const int nstr = (B - c0 - IB) / 16;
+    // One code path for both panel types (16-B paired-row sc1 strip accesses; head rows through
+    // a buffer resource): GEQRT's explicit V (zeros above the unit diagonal) under the TSQRT
+    // stream with a zero head is exactly the GE update; its 8-row blocks above the group are
+    // neither loaded nor stored (finished R rows, which the next member's trailing may be
+    // updating meanwhile); the head resource is empty for GEQRT (loads 0, stores dropped) —
+    // see flow_chain's UNMQR element.
+    const __amdgpu_buffer_rsrc_t rsH = head_rsrc(Rt, !qrs);
+    const int h0 = qrs ? c0 / 8 : 0;
     for (int s = w; s < nstr; s += FLOW_NT / 64) {
       asm volatile("" ::: "memory");
       const int col = c0 + IB + 16 * s;
-      if (qrs) {
-        load_strip<B, S, true>(X, Rt, ldm, col, ks0);
-        apply_group<B, false, FLOW_PF, true>(Vs, Tp, X, H, ks0);
-        store_strip<B>(X, Rt, ldm, col, ks0);
-      } else {
-        load_strip<B, S, true>(X, Bt, ldm, col, 0);
-        load_head<B, S, true>(H, Rt, ldm, c0, col);
-        apply_group<B, true, FLOW_PF, true>(Vs, Tp, X, H, 0);
-        store_strip<B>(X, Bt, ldm, col, 0);
-        store_head<B>(H, Rt, ldm, c0, col);
-      }
+      const unsigned so = head_off<B, S>(ldm, c0, col);  // head row c0 + x, column col + lane's
+      load_strip_pair<B, S>(X, Bt, ldm, col, h0);
+      load_head_buf<B, S, 16>(H, rsH, so);
+#ifdef TQR_FLOW_STAMPS
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      FST(16);
+      apply_group<B, true, FLOW_PF, true>(Vs, Tp, X, H, 0);
+      FST(12);
+      store_strip_pair<B, S>(X, Bt, ldm, col, h0);
+      store_head_buf<B, S, 16>(H, rsH, so);
+      FST(17);
     }
     wg_publish(&a.Rt[(size_t)k * NG + g], 1);
     FST(12);

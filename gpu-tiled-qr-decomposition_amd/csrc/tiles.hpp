@@ -306,8 +306,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, 0x7fffffff, 0x00020000);
 }
 __device__ __forceinline__ int vimg_row(int q) { return 8 * (q >> 3) + 2 * (q & 3) + ((q >> 2) & 1); }
+// inverse: tile row r -> image row
+__device__ __forceinline__ int vimg_inv(int r) { return 8 * (r >> 3) + 4 * (r & 1) + ((r >> 1) & 3); }
+// h0: 8-row blocks above it are neither loaded (zero) nor stored (the GEQRT panel's finished
+// R rows, which other members' trailing updates may be writing meanwhile)
 template <int B, typename S>
-__device__ __forceinline__ void load_strip_pair(double (&X)[Geo<B>::NKS], S* tile, size_t ldm, int col0) {
+__device__ __forceinline__ void load_strip_pair(double (&X)[Geo<B>::NKS], S* tile, size_t ldm, int col0, int h0 = 0) {
   const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
   __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile);
   const unsigned base = (unsigned)(((size_t)c * ldm + 2 * x) * sizeof(S));
@@ -315,6 +319,10 @@ __device__ __forceinline__ void load_strip_pair(double (&X)[Geo<B>::NKS], S* til
   // unsigned voffset + constant cannot be folded into the immediate field without a no-wrap proof)
 #pragma unroll
   for (int h = 0; h < Geo<B>::NKS / 2; ++h) {
+    if (h < h0) {
+      X[2 * h] = X[2 * h + 1] = 0.0;
+      continue;
+    }
     const int so = 8 * h * sizeof(S);
     if constexpr (sizeof(S) == 8) {
       auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, base, so, 16);
@@ -328,12 +336,14 @@ __device__ __forceinline__ void load_strip_pair(double (&X)[Geo<B>::NKS], S* til
   }
 }
 template <int B, typename S>
-__device__ __forceinline__ void store_strip_pair(const double (&X)[Geo<B>::NKS], S* tile, size_t ldm, int col0) {
+__device__ __forceinline__ void store_strip_pair(const double (&X)[Geo<B>::NKS], S* tile, size_t ldm, int col0,
+                                                 int h0 = 0) {
   const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
   __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile);
   const unsigned base = (unsigned)(((size_t)c * ldm + 2 * x) * sizeof(S));
 #pragma unroll
   for (int h = 0; h < Geo<B>::NKS / 2; ++h) {
+    if (h < h0) continue;
     const int so = 8 * h * sizeof(S);
     if constexpr (sizeof(S) == 8) {
       const unsigned long long a = (unsigned long long)__double_as_longlong(X[2 * h]);
@@ -384,6 +394,39 @@ __device__ __forceinline__ void store_head_buf(const double (&H)[Geo<B>::NRI], _
       __builtin_amdgcn_raw_buffer_store_b64(v, rs, base, 4 * r * 8, AUX);
     } else {
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)H[r]), rs, base, 4 * r * 4, AUX);
+    }
+  }
+}
+// Natural-order strip through a buffer resource (the panel's in-tile trailing update):
+// X[ks] <- tile(row 4ks + x, column col0 + 4blk + y), rows < 4*ks0 zero (not loaded / stored).
+// Buffer (not FLAT) accesses keep the LDS counter free for the MFMA operand waits.
+template <int B, typename S, int AUX>
+__device__ __forceinline__ void load_strip_buf(double (&X)[Geo<B>::NKS], __amdgpu_buffer_rsrc_t rs, unsigned base,
+                                               int ks0) {
+#pragma unroll
+  for (int ks = 0; ks < Geo<B>::NKS; ++ks) {
+    if (ks < ks0) {
+      X[ks] = 0.0;
+    } else if constexpr (sizeof(S) == 8) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, base, 4 * ks * 8, AUX);
+      X[ks] = __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
+    } else {
+      X[ks] = (double)__uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, base, 4 * ks * 4, AUX));
+    }
+  }
+}
+template <int B, typename S, int AUX>
+__device__ __forceinline__ void store_strip_buf(const double (&X)[Geo<B>::NKS], __amdgpu_buffer_rsrc_t rs, unsigned base,
+                                                int ks0) {
+#pragma unroll
+  for (int ks = 0; ks < Geo<B>::NKS; ++ks) {
+    if (ks < ks0) continue;
+    if constexpr (sizeof(S) == 8) {
+      const unsigned long long u = (unsigned long long)__double_as_longlong(X[ks]);
+      __attribute__((ext_vector_type(2))) unsigned v = {(unsigned)u, (unsigned)(u >> 32)};
+      __builtin_amdgcn_raw_buffer_store_b64(v, rs, base, 4 * ks * 8, AUX);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)X[ks]), rs, base, 4 * ks * 4, AUX);
     }
   }
 }
@@ -578,13 +621,13 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 //   5. rows update x_j -= f_j v (tails) / head_j -= f_j (GE head row, TS head in `hout`).
 template <int B, bool TS, int NW>
 __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, double* Hs, double* tauv, double* red,
-                                           double* wb, double* hrow, double* hout, int c0, int C, bool own) {
+                                           double* wb, double* hrow, double* hout, int c0, int C, bool own, int rt) {
   using g = Geo<B>;
   constexpr int IB = g::IB, TP = g::TP, VP = g::VP;
   constexpr int SPAN = 64 / NW;  // lanes holding the same column after reduce-scatter
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int rc = c0 + C;  // GE: tile row of the reflector head
-  const bool tail = own && (TS || t > rc);
+  const bool tail = own && (TS || rt > rc);  // rt: the tile row this thread holds
   double pv[NW];
 #pragma unroll
   for (int j = 0; j < NW; ++j) pv[j] = tail ? x[0] * x[j] : 0.0;
@@ -594,7 +637,7 @@ __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, 
   const bool wr = (lane & (SPAN - 1)) == 0;
   double* rb = red + (C & 1) * 128;
   if (wr && w < 4) rb[w * 32 + cr] = ws;  // rows live in waves 0-3
-  if (!TS && t == rc) {
+  if (!TS && rt == rc) {
 #pragma unroll
     for (int j = 0; j < NW; ++j) hrow[(C & 1) * 32 + j] = x[j];
   }
@@ -625,7 +668,7 @@ __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, 
 #pragma unroll
     for (int j = 1; j < NW; ++j) x[j] = fma(-f[j], xc, x[j]);
     x[0] = xc;
-  } else if (!TS && t == rc) {
+  } else if (!TS && rt == rc) {
 #pragma unroll
     for (int j = 1; j < NW; ++j) x[j] -= f[j];
     x[0] = x0 - f[0];
@@ -638,7 +681,9 @@ __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, 
   x[NW - 1] = 0.0;
 }
 
-template <int B, bool TS>
+// PERM: LDS row q of Vs holds tile row vimg_row(q) (the chain engine's paired row order), else
+// tile row q.
+template <int B, bool TS, bool PERM = false>
 __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, double* scratch, int c0) {
   using g = Geo<B>;
   constexpr int IB = g::IB, VP = g::VP, TP = g::TP;
@@ -656,17 +701,18 @@ __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, 
     if (TS) __syncthreads();
     return;
   }
-  const bool own = t < B && (TS || t >= c0);
+  const int rt = PERM ? vimg_row(t) : t;
+  const bool own = t < B && (TS || rt >= c0);
   double x[IB];
 #pragma unroll
   for (int j = 0; j < IB; ++j) x[j] = own ? Vs[t * VP + g::pc(j)] : 0.0;
   // reduce the live window only: all IB columns while more than IB/2 are live, then the half
   constexpr int HALF = IB == 32 ? 16 : IB;
 #pragma clang loop unroll(disable)
-  for (int C = 0; C < HALF; ++C) panel_step<B, TS, IB>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own);
+  for (int C = 0; C < HALF; ++C) panel_step<B, TS, IB>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
   if constexpr (HALF < IB) {
 #pragma clang loop unroll(disable)
-    for (int C = HALF; C < IB; ++C) panel_step<B, TS, IB / 2>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own);
+    for (int C = HALF; C < IB; ++C) panel_step<B, TS, IB / 2>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
   }
   __syncthreads();
   if (TS) {
