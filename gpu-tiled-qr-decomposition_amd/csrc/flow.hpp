@@ -302,6 +302,33 @@ struct PanelView {
   }
 };
 
+// Two consecutive elements (a row pair of a column) as one sc1 buffer access: 16 B for fp64,
+// 8 B for fp32 storage.
+template <typename S>
+__device__ __forceinline__ void ld_pair(__amdgpu_buffer_rsrc_t rs, unsigned off, double& a, double& b) {
+  if constexpr (sizeof(S) == 8) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+    a = __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
+    b = __longlong_as_double((long long)(((unsigned long long)v[3] << 32) | v[2]));
+  } else {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 16);
+    a = (double)__uint_as_float(v[0]);
+    b = (double)__uint_as_float(v[1]);
+  }
+}
+template <typename S>
+__device__ __forceinline__ void st_pair(__amdgpu_buffer_rsrc_t rs, unsigned off, double a, double b) {
+  if constexpr (sizeof(S) == 8) {
+    const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
+    const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
+    __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)ua, (unsigned)(ua >> 32), (unsigned)ub, (unsigned)(ub >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);
+  } else {
+    __attribute__((ext_vector_type(2))) unsigned v = {__float_as_uint((float)a), __float_as_uint((float)b)};
+    __builtin_amdgcn_raw_buffer_store_b64(v, rs, off, 0, 16);
+  }
+}
+
 // ---- panel tasks ---------------------------------------------------------------------------
 template <int B, typename S>
 __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* lds, int* sflag) {
@@ -341,18 +368,19 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       if (!wg_verdict(ok, sflag)) return;
       FST(1);
     }
-    if (qrs) {
-#pragma unroll 8
-      for (int idx = t; idx < B * IB; idx += FLOW_NT) {
-        const int r = idx % B, c = idx / B;
-        Vs[vimg_inv(r) * VP + G::pc(c)] = r >= c0 ? ldc(Rt + (size_t)(c0 + c) * ldm + r) : 0.0;
+    {  // the group's B x IB block, row pairs as 16-B sc1 buffer loads (GEQRT: rows above c0 zero)
+      const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt);
+      const int rlo = qrs ? c0 : 0;
+#pragma unroll 4
+      for (int idx = t; idx < B * IB / 2; idx += FLOW_NT) {
+        const int r = 2 * (idx % (B / 2)), c = idx / (B / 2);
+        double v0 = 0.0, v1 = 0.0;
+        if (r >= rlo) ld_pair<S>(rs, (unsigned)(((size_t)(c0 + c) * ldm + r) * sizeof(S)), v0, v1);
+        Vs[vimg_inv(r) * VP + G::pc(c)] = v0;
+        Vs[vimg_inv(r + 1) * VP + G::pc(c)] = v1;
       }
-    } else {
-#pragma unroll 8
-      for (int idx = t; idx < B * IB; idx += FLOW_NT) {
-        const int r = idx % B, c = idx / B;
-        Vs[vimg_inv(r) * VP + G::pc(c)] = ldc(Bt + (size_t)(c0 + c) * ldm + r);
-      }
+    }
+    if (!qrs) {
       for (int idx = t; idx < IB * IB; idx += FLOW_NT) {
         const int r = idx % IB, c = idx / IB;
         if (r <= c) Hs[r * TP + c] = ldc(Rt + (size_t)(c0 + c) * ldm + c0 + r);
@@ -365,16 +393,18 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     if (qrs) panel_factor<B, false, true>(Vs, Hs, tauv, scratch, c0);
     else panel_factor<B, true, true>(Vs, Hs, tauv, scratch, c0);
     FST(5);
-    if (qrs) {
-      for (int idx = t; idx < B * IB; idx += FLOW_NT) {
-        const int r = idx % B, c = idx / B;
-        if (r >= c0) st(Rt + (size_t)(c0 + c) * ldm + r, Vs[vimg_inv(r) * VP + G::pc(c)]);
+    {  // write-back of the factored block (R / V), row pairs as 16-B write-through stores
+      const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt);
+      const int rlo = qrs ? c0 : 0;
+#pragma unroll 4
+      for (int idx = t; idx < B * IB / 2; idx += FLOW_NT) {
+        const int r = 2 * (idx % (B / 2)), c = idx / (B / 2);
+        if (r >= rlo)
+          st_pair<S>(rs, (unsigned)(((size_t)(c0 + c) * ldm + r) * sizeof(S)), Vs[vimg_inv(r) * VP + G::pc(c)],
+                     Vs[vimg_inv(r + 1) * VP + G::pc(c)]);
       }
-    } else {
-      for (int idx = t; idx < B * IB; idx += FLOW_NT) {
-        const int r = idx % B, c = idx / B;
-        st(Bt + (size_t)(c0 + c) * ldm + r, Vs[vimg_inv(r) * VP + G::pc(c)]);
-      }
+    }
+    if (!qrs) {
       for (int idx = t; idx < IB * IB; idx += FLOW_NT) {
         const int r = idx % IB, c = idx / IB;
         if (r <= c) st(Rt + (size_t)(c0 + c) * ldm + c0 + r, Hs[r * TP + c]);
@@ -399,8 +429,9 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     {  // V image (explicit) and packed T image of this group for the chains (LDS-DMA sources)
       double* tg = flow_tw<B>(a, qrs ? k : l, k, g);
       double* vg = flow_vw<B>(a, qrs ? k : l, k, g);
-      for (int idx = t; idx < G::TPIMG; idx += FLOW_NT) st(tg + idx, Tp[idx]);
-      for (int idx = t; idx < G::VSZ; idx += FLOW_NT) st(vg + idx, Vs[idx]);
+      const __amdgpu_buffer_rsrc_t rv = uniform_rsrc(vg), rt = uniform_rsrc(tg);
+      for (int idx = t; idx < G::TPIMG / 2; idx += FLOW_NT) st_pair<double>(rt, 16 * idx, Tp[2 * idx], Tp[2 * idx + 1]);
+      for (int idx = t; idx < G::VSZ / 2; idx += FLOW_NT) st_pair<double>(rv, 16 * idx, Vs[2 * idx], Vs[2 * idx + 1]);
     }
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
     wg_publish(&a.Rc[(size_t)k * NG + g], 1);
