@@ -252,6 +252,23 @@ __device__ __forceinline__ bool sync_point(bool ok0, int* sflag, int& par) {
   asm volatile("" ::: "memory");
   return *(volatile int*)slot != 0;
 }
+// The first group's sync point of an element: everything older than the element's own strip and
+// head loads (the previous element's stores, this group's LDS-DMA) must be complete, the NX
+// loads issued after them need not be — phase 1 waits for each strip row as it reaches it (the
+// compiler's vmcnt per use; the LDS-DMA of the next group, issued in between, only makes those
+// waits conservative). A wave without loads (strip past the tile) drains fully.
+template <int NX>
+__device__ __forceinline__ bool sync_point_first(bool ok0, int* sflag, int& par, bool loaded) {
+  int* slot = sflag + 40 + par;
+  par ^= 1;
+  if (threadIdx.x == 0) *slot = ok0 ? 1 : 0;
+  static_assert(NX >= 0 && NX < 64, "vmcnt range");
+  if (loaded) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NX) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  return *(volatile int*)slot != 0;
+}
 // thread 0, after a draining sync point (every wave's sc1 stores complete): bump a counter
 __device__ __forceinline__ void publish_after_drain(int* p, int delta) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(gptr(p), delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -583,14 +600,14 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     }
     FST(7);
     S* Xt = ts ? A + (size_t)j * B * ldm + (size_t)i * B : At;
-#ifndef TQR_DIAG_NOSTRIP
-    if (active) load_strip_pair<B, S>(X, Xt, ldm, col);
-#endif
-    if (!dma_next) {
+    if (!dma_next) {  // (first: the strip and head loads must be the youngest, see sync_point_first)
       DmaJob<B> d{lds + buf * BUF, vimg(i, 0), timg(i, 0), sflag};
       for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
     }
     dma_next = false;
+#ifndef TQR_DIAG_NOSTRIP
+    if (active) load_strip_pair<B, S>(X, Xt, ldm, col);
+#endif
     // head rows: written by another workgroup before this segment or by this one (sc1 loads
     // for both). The UNMQR element (i == k, GE-type V) runs the very same TSMQR code with a zero
     // head: its V image is explicit (zeros above the unit diagonal), so Z = 0 + V^T X and X += V W
@@ -614,7 +631,10 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
           else if (has_next) ok = ready(inext, 0);
         }
         FST(0);
-        if (!sync_point<true>(ok, sflag, par)) return false;
+        // group 0: the strip / head loads of this element may still be in flight
+        constexpr int NX = G::NKS / 2 + (FLOW_PF ? G::NRI : 0);
+        if (!(g == 0 ? sync_point_first<NX>(ok, sflag, par, active) : sync_point<true>(ok, sflag, par)))
+          return false;
       }
       if (g == 0 && pending) {
         publish_after_drain(pending, 1);

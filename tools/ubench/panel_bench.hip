@@ -1,0 +1,60 @@
+// Microbenchmark: latency of one reflector group of the TSQRT / GEQRT panel (tiles.hpp
+// panel_factor, 32 reflectors on a 256-row block in LDS) at 256 and 512 threads per workgroup,
+// one workgroup per CU, no global traffic. Prints us per group.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include "tiles.hpp"
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+using namespace tqr;
+constexpr int B = 256;
+using G = Geo<B>;
+constexpr int LDS_D = G::VSZ + 2 * G::TSZ + G::IB + 2 + 2 * 4 * 32 + 4 * 32 + 2 * 32 + G::TSZ;
+
+template <bool TS, int NTH>
+__global__ __launch_bounds__(NTH, 1) void k_panel(double* out, int iters) {
+  extern __shared__ __align__(16) double lds[];
+  double* Vs = lds;
+  double* Hs = Vs + G::VSZ;
+  double* tauv = Hs + G::TSZ;
+  double* scratch = tauv + G::IB + 2;
+  for (int i = threadIdx.x; i < LDS_D; i += NTH) lds[i] = 1e-2 * ((i * 37) % 101 - 50) + (i % 35 == 0 ? 1.0 : 0.0);
+  __syncthreads();
+  for (int it = 0; it < iters; ++it) panel_factor<B, TS, true>(Vs, Hs, tauv, scratch, TS ? 0 : 32 * (it & 3));
+  __syncthreads();
+  if (threadIdx.x < 64) out[blockIdx.x * 64 + threadIdx.x] = Vs[threadIdx.x] + tauv[threadIdx.x & 31];
+}
+
+template <bool TS, int NTH>
+static int run(const char* name, double* out, int blocks) {
+  const size_t lds = LDS_D * sizeof(double);
+  CK(hipFuncSetAttribute((const void*)k_panel<TS, NTH>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int iters = 400;
+  k_panel<TS, NTH><<<blocks, NTH, lds>>>(out, 4);
+  CK(hipDeviceSynchronize());
+  float ms;
+  CK(hipEventRecord(e0));
+  k_panel<TS, NTH><<<blocks, NTH, lds>>>(out, iters);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  printf("%-8s %3d threads: %7.2f us per group (%5.3f us per reflector)\n", name, NTH, ms * 1e3 / iters,
+         ms * 1e3 / iters / G::IB);
+  return 0;
+}
+
+int main() {
+  hipDeviceProp_t p;
+  CK(hipGetDeviceProperties(&p, 0));
+  double* out;
+  CK(hipMalloc(&out, p.multiProcessorCount * 64 * sizeof(double)));
+  for (int blocks : {1, p.multiProcessorCount}) {
+    printf("-- %d workgroup(s)\n", blocks);
+    if (run<true, 256>("TSQRT", out, blocks) || run<true, 512>("TSQRT", out, blocks) ||
+        run<false, 256>("GEQRT", out, blocks) || run<false, 512>("GEQRT", out, blocks))
+      return 1;
+  }
+  return 0;
+}
