@@ -60,6 +60,7 @@ __device__ unsigned long long g_pstamps[8];
 
 #ifdef TQR_FLOW_STAMPS
 __device__ unsigned long long g_fst[4096 * 24];  // >= FST_N categories per workgroup
+__device__ unsigned long long g_ttl[3 << 18];     // task timeline (first 2^18 tasks)
 #endif
 }  // namespace tqr
 #include "flow.hpp"
@@ -723,7 +724,8 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
-    pl->sync_ints = 2 + 3 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns + (size_t)pl->kmax * pl->q * pl->ns;
+    pl->sync_ints = 2 + 3 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns +
+                    (size_t)pl->kmax * pl->q * pl->ns * pl->ng;
     if (pl->nflow <= 0 || hipMalloc(&pl->d_flow, sizeof(Item) * pl->nflow) != hipSuccess ||
         hipMalloc(&pl->d_sync, sizeof(int) * pl->sync_ints) != hipSuccess ||
         hipMalloc(&pl->d_wk, sizeof(double*) * pl->kmax) != hipSuccess) {
@@ -899,7 +901,7 @@ int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream)
     f.next = pl->d_sync; f.err = pl->d_sync + 1; f.Rc = pl->d_sync + 2;
     f.Tc = f.Rc + (size_t)pl->kmax * pl->ng;
     f.Ac = f.Tc + (size_t)pl->p * pl->q * pl->ns;
-    f.Rt = f.Ac + (size_t)pl->kmax * pl->q * pl->ns;
+    f.Rt = f.Ac + (size_t)pl->kmax * pl->q * pl->ns * pl->ng;
     f.Rr = f.Rt + (size_t)pl->kmax * pl->ng;
     f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.peers = pl->d_peers; f.Rf = pl->d_rf;
     // multi-GPU: counters and flags are reset by tqr_dist_reset (all ranks, then a barrier)
@@ -1190,6 +1192,14 @@ extern "C" int tqr_debug_stamps(unsigned long long* out, int reset) {
 extern "C" int tqr_debug_flow_stamps(unsigned long long* out, int nblocks) {
   if (nblocks > 4096) return TQR_EINVAL;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fst), sizeof(unsigned long long) * FST_N * nblocks) != hipSuccess) return TQR_EHIP;
+  return TQR_OK;
+}
+// task timeline of the last k_flow launch: (start, end, workgroup) per task index, and the task list
+extern "C" int tqr_debug_task_timeline(const tqr_plan* plan, unsigned long long* out, int ntasks, int* items) {
+  if (ntasks > (1 << 18)) return TQR_EINVAL;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ttl), sizeof(unsigned long long) * 3 * ntasks) != hipSuccess) return TQR_EHIP;
+  if (items && plan->d_flow && hipMemcpy(items, plan->d_flow, sizeof(Item) * ntasks, hipMemcpyDeviceToHost) != hipSuccess)
+    return TQR_EHIP;
   return TQR_OK;
 }
 #endif

@@ -22,7 +22,8 @@
 //              TSQRT's group g may start once its predecessor finished group g, so the flat
 //              TS chain is pipelined at group (32-reflector) granularity, not tile granularity;
 //   Tc[i][j][s] steps completed on strip s of tile (i,j);
-//   Ac[k][j][s] segments completed of chain (k,j,s).
+//   Ac[k][j][s][g] segments of chain (k,j,s) whose head rows of group g are final (the next
+//                 segment starts group g of its first element on it).
 // Deadlock freedom: every wait is on a task earlier in the list (host checks it), and tasks are
 // dequeued in list order, so the earliest unfinished dequeued task can always progress. Every
 // spin is bounded (FLOW_TIMEOUT); on timeout an error word is set and all workgroups drain.
@@ -47,6 +48,7 @@ constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel memb
 constexpr int FST_N = 18;
 #ifdef TQR_FLOW_STAMPS
 extern __device__ unsigned long long g_fst[];
+extern __device__ unsigned long long g_ttl[];  // per task: start, end (s_memrealtime), workgroup
 #define FST(c)                                                                            \
   do {                                                                                    \
     if (threadIdx.x == 0) {                                                               \
@@ -560,7 +562,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B>(P, i_, k, g_); };
   auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B>(P, i_, k, g_); };
   int* const rc = &a.Rc[(size_t)k * NG];
-  int* const ac = &a.Ac[((size_t)k * Q + j) * NS + s];
+  int* const acg = &a.Ac[(((size_t)k * Q + j) * NS + s) * NG];  // per head-row group
   auto tc = [&](int i) { return &Tc[((size_t)i * Q + j) * NS + s]; };
   double X[G::NKS];
   double H[G::NRI], Hn[G::NRI], W[G::NRI];
@@ -588,7 +590,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     {
       bool ok = true;
       if (t == 0) {
-        if (i == ifirst && seg > 0) ok = spin_ge(ac, seg, err);
+        if (i == ifirst && seg > 0) ok = spin_ge(&acg[0], seg, err);
         FST(9);
         if (ok && k > 0 && tc_pf < k) ok = spin_ge(tc(i), k, err);
         tc_pf = -1;
@@ -627,8 +629,12 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       {
         bool ok = true;
         if (t == 0) {
-          if (g + 1 < NG) ok = ready(i, g + 1);
-          else if (has_next) ok = ready(inext, 0);
+          // first element of a later segment: head rows of group g+1 (prefetched below) final?
+          if (i == ifirst && seg > 0 && g + 1 < NG) ok = spin_ge(&acg[g + 1], seg, err);
+          if (ok) {
+            if (g + 1 < NG) ok = ready(i, g + 1);
+            else if (has_next) ok = ready(inext, 0);
+          }
         }
         FST(0);
         // group 0: the strip / head loads of this element may still be in flight
@@ -640,6 +646,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         publish_after_drain(pending, 1);
         pending = nullptr;
       }
+      // segment's last element: its head rows of group g-1 (stored write-through) are drained
+      if (!has_next && g > 0) publish_after_drain(&acg[g - 1], 1);
       if (t == 0) {  // early loads of the counters the next sync point will test
         if (!remote) {
           pv.prefetch(rc, false);
@@ -673,9 +681,11 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       FST(15);
 #ifndef TQR_DIAG_NOHEAD
       if (active) {
-        // head rows stay with this workgroup for the whole segment: plain (write-back) stores,
-        // made visible to the next segment's workgroup by one release before the Ac publish
-        store_head_buf<B, S, 0>(H, hrs, hoff + g * IB * sizeof(S));
+        // head rows stay with this workgroup inside the segment (plain write-back stores); the
+        // segment's last element hands them to the next segment group by group: write-through
+        // stores, drained, then Ac[k][j][s][g]++ (one group later, after the next drain)
+        if (has_next) store_head_buf<B, S, 0>(H, hrs, hoff + g * IB * sizeof(S));
+        else store_head_buf<B, S, 16>(H, hrs, hoff + g * IB * sizeof(S));
         FST(2);
         if (FLOW_PF && g + 1 < NG) load_head_buf<B, S, 16>(Hn, hrs, hoff + (g + 1) * IB * sizeof(S));
       }
@@ -698,11 +708,10 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     pending = tc(i);
     FST(4);
   }
-  // last element's strip and the segment: drain, then publish both
+  // last element's strip and its last head-row group: drain, then publish both
   sync_point<true>(true, sflag, par);
   if (pending) publish_after_drain(pending, 1);
-  if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the plain-stored head rows
-  publish_after_drain(ac, 1);
+  publish_after_drain(&acg[NG - 1], 1);
   FST(4);
 }
 
@@ -740,6 +749,12 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
     if (idx >= a.ntasks) break;
     const Item it = a.tasks[idx];
     const int type = it.ts & 0xff;
+#ifdef TQR_FLOW_STAMPS
+    if (threadIdx.x == 0 && idx < (1 << 18)) {
+      g_ttl[3 * idx] = __builtin_amdgcn_s_memrealtime();
+      g_ttl[3 * idx + 2] = blockIdx.x;
+    }
+#endif
     if (type == T_CHAIN) {
       flow_chain<B, S>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                        s_flag);
@@ -749,6 +764,9 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
       flow_panel<B, S>(a, type, it.l, it.k, lds, s_flag);
     }
     __syncthreads();
+#ifdef TQR_FLOW_STAMPS
+    if (threadIdx.x == 0 && idx < (1 << 18)) g_ttl[3 * idx + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
   }
 #ifdef TQR_FLOW_STAMPS
   FST(6);

@@ -1,0 +1,51 @@
+"""Diagnostic: task timeline of the persistent engine (libtqr_fst.so): per factorisation step k,
+when its panel and its chains start and end, and how many workgroups hold a task over time.
+Usage: python tools/timeline.py [m] [b]"""
+import ctypes, os, sys
+import numpy as np
+import torch
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpu-tiled-qr-decomposition_amd"))
+import tqr
+tqr.LIB_PATH = tqr.LIB_PATH.replace("libtqr.so", os.environ.get("TQR_FST_LIB", "libtqr_fst.so"))
+L = tqr.lib()
+m = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+b = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+A = torch.empty((m, m), dtype=torch.float64, device="cuda")
+tau = torch.zeros((m // b, m), dtype=torch.float64, device="cuda")
+p = tqr.TiledQR(m, m, b, torch.float64)
+for rep in range(2):
+    tqr.fill_randzo(A, m, m, 5)
+    p.execute(A, tau)
+    torch.cuda.synchronize()
+eng, nt, est, grid = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+L.tqr_plan_info(p.h, ctypes.byref(eng), ctypes.byref(nt), ctypes.byref(est), ctypes.byref(grid))
+n = nt.value
+tl = (ctypes.c_ulonglong * (3 * n))()
+items = (ctypes.c_int * (4 * n))()
+assert L.tqr_debug_task_timeline(p.h, tl, n, items) == 0
+T = np.frombuffer(tl, dtype=np.uint64).reshape(n, 3).astype(np.int64)
+I = np.frombuffer(items, dtype=np.int32).reshape(n, 4)
+t0 = T[:, 0].min()
+s = (T[:, 0] - t0) / 100.0  # us (100 MHz)
+e = (T[:, 1] - t0) / 100.0
+typ = I[:, 0] & 0xff
+k = np.where(typ == 4, I[:, 3] & 0xffff, I[:, 3])
+chain = typ == 4
+print(f"{m}^2 b={b}: {n} tasks, launch span {e.max() / 1e3:.1f} ms, {grid.value} workgroups")
+print(" step  panel start..end (ms)   chains start..end (ms)   chain tasks")
+K = m // b
+for kk in list(range(0, K, 4)) + [K - 1]:
+    pm = (k == kk) & ~chain
+    cm = (k == kk) & chain
+    ps = f"{s[pm].min() / 1e3:7.2f}..{e[pm].max() / 1e3:7.2f}" if pm.any() else "   -   "
+    cs = f"{s[cm].min() / 1e3:7.2f}..{e[cm].max() / 1e3:7.2f}" if cm.any() else "   -   "
+    print(f" {kk:4d}  {ps}        {cs}      {cm.sum():5d}")
+# workgroups holding a task, per 5 % of the span
+span = e.max()
+print(" occupancy (mean workgroups holding a task) per 5 % of the launch:")
+edges = np.linspace(0, span, 21)
+occ = []
+for a0, a1 in zip(edges[:-1], edges[1:]):
+    ov = np.clip(np.minimum(e, a1) - np.maximum(s, a0), 0, None).sum() / (a1 - a0)
+    occ.append(ov)
+print("  " + " ".join(f"{o:5.0f}" for o in occ))
