@@ -43,6 +43,16 @@ extern __device__ unsigned long long g_pstamps[8];
 #define PSTAMP(i) do {} while (0)
 #define PSTAMP_INIT
 #endif
+// build_t phase stamps (tools/ubench/panel_bench.hip only)
+#ifdef TQR_BT_STAMPS
+extern __device__ unsigned long long g_bt[8];
+#define BT_STAMP(i)                                                                          \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(&g_bt[i], (unsigned long long)__builtin_amdgcn_s_memtime()); \
+  } while (0)
+#else
+#define BT_STAMP(i) do {} while (0)
+#endif
 
 constexpr int NT = 256;  // threads per workgroup (4 waves)
 
@@ -740,7 +750,33 @@ __device__ __noinline__ void build_t(const double* Vs, const double* tauv, doubl
   constexpr int KPW = (NKS + 3) / 4;  // k-steps per wave
   constexpr int NCH = IB / 16;        // 16-column halves of the Gram
   const int t = threadIdx.x, w = t >> 6, lane = t & 63, x = lane >> 4, y = lane & 3, blk = (lane >> 2) & 3;
-  {
+  BT_STAMP(0);
+  if (blockDim.x >= 512 && NCH == 2) {
+    // 8 waves: wave w sums rows of k-step block (w & 3) into Gram column half (w >> 2)
+    const int h = w >> 2;
+    double Z[NRI];
+#pragma unroll
+    for (int r = 0; r < NRI; ++r) Z[r] = 0.0;
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+      const int ks = (w & 3) * KPW + kk;
+      if (ks >= NKS || ks < ks0) continue;
+      const double2* vr = reinterpret_cast<const double2*>(Vs + (4 * ks + x) * VP + y * NRI);
+      double a[NRI];
+#pragma unroll
+      for (int q = 0; q < NRI / 2; ++q) {
+        double2 tt = vr[q];
+        a[2 * q] = tt.x;
+        a[2 * q + 1] = tt.y;
+      }
+      const double xb = Vs[(4 * ks + x) * VP + g::pc(16 * h + 4 * blk + y)];
+#pragma unroll
+      for (int r = 0; r < NRI; ++r) Z[r] = mfma4(a[r], xb, Z[r]);
+    }
+    double* gp = Gp + (w & 3) * IB * TP;
+#pragma unroll
+    for (int r = 0; r < NRI; ++r) gp[(4 * r + x) * TP + 16 * h + 4 * blk + y] = Z[r];
+  } else {
     double Z[NCH][NRI];
 #pragma unroll
     for (int h = 0; h < NCH; ++h)
@@ -773,11 +809,13 @@ __device__ __noinline__ void build_t(const double* Vs, const double* tauv, doubl
       for (int r = 0; r < NRI; ++r) gp[(4 * r + x) * TP + 16 * h + 4 * blk + y] = Z[h][r];
   }
   __syncthreads();
+  BT_STAMP(1);
   for (int idx = t; idx < IB * IB; idx += blockDim.x) {
     const int r = idx / IB, c = idx % IB, o = r * TP + c;
     Gs[o] = (Gp[o] + Gp[IB * TP + o]) + (Gp[2 * IB * TP + o] + Gp[3 * IB * TP + o]);
   }
   __syncthreads();
+  BT_STAMP(2);
   // back substitution: column j = t >> 3 (t < 8*IB), lane e = t & 7 holds x_k, k = e + 8q
   constexpr int NQ = IB / 8;
   const int j = t >> 3, e = t & 7;
@@ -790,13 +828,19 @@ __device__ __noinline__ void build_t(const double* Vs, const double* tauv, doubl
       double part = 0.0;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
+        // the Gram entry is read unconditionally (always in range) and masked by a select: a
+        // conditional read became a divergent branch with its own LDS wait per (i, q)
         const int k = e + 8 * q;
-        part += (k > i && k <= j) ? Gs[i * TP + k] * xr[q] : 0.0;
+        double gv = Gs[i * TP + k];
+        asm("" : "+v"(gv));  // keeps the read unconditional (else it is sunk into a branch)
+        part += ((k > i && k <= j) ? gv : 0.0) * xr[q];
       }
       part += dpp<DPP_ROW_HALF_MIRROR>(part);
       part += dpp<DPP_QUAD_3210>(part);
       part += dpp<DPP_QUAD_1032>(part);
-      if (i < j && e == (i & 7)) xr[i >> 3] = -tauv[i] * part;
+      double ti = tauv[i];
+      asm("" : "+v"(ti));
+      if (i < j && e == (i & 7)) xr[i >> 3] = -ti * part;
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -805,6 +849,7 @@ __device__ __noinline__ void build_t(const double* Vs, const double* tauv, doubl
     }
   }
   __syncthreads();
+  BT_STAMP(3);
 }
 
 }  // namespace tqr

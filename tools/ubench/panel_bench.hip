@@ -3,7 +3,9 @@
 // one workgroup per CU, no global traffic. Prints us per group.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#define TQR_BT_STAMPS
 #include "tiles.hpp"
+namespace tqr { __device__ unsigned long long g_bt[8]; }
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 using namespace tqr;
 constexpr int B = 256;
@@ -22,6 +24,55 @@ __global__ __launch_bounds__(NTH, 1) void k_panel(double* out, int iters) {
   for (int it = 0; it < iters; ++it) panel_factor<B, TS, true>(Vs, Hs, tauv, scratch, TS ? 0 : 32 * (it & 3));
   __syncthreads();
   if (threadIdx.x < 64) out[blockIdx.x * 64 + threadIdx.x] = Vs[threadIdx.x] + tauv[threadIdx.x & 31];
+}
+
+template <int NTH>
+__global__ __launch_bounds__(NTH, 1) void k_buildt(double* out, int iters) {
+  extern __shared__ __align__(16) double lds[];
+  double* Vs = lds;
+  double* tauv = Vs + G::VSZ;
+  double* Gs = tauv + G::IB + 2;
+  double* Ts = Gs + G::TSZ;
+  double* Gp = Ts + G::TSZ;
+  for (int i = threadIdx.x; i < G::VSZ + G::IB + 2; i += NTH) lds[i] = 1e-2 * ((i * 37) % 101 - 50) + 1.0;
+  __syncthreads();
+  for (int it = 0; it < iters; ++it) {
+    build_t<B>(Vs, tauv, Gs, Ts, Gp, 0);
+    pack_t<B, NTH>(Ts, Gs);
+    __syncthreads();
+  }
+  if (threadIdx.x < 64) out[blockIdx.x * 64 + threadIdx.x] = Gs[threadIdx.x];
+}
+
+template <int NTH>
+static int run_bt(double* out, int blocks) {
+  const size_t lds = (G::VSZ + G::IB + 2 + 6 * G::TSZ) * sizeof(double);
+  CK(hipFuncSetAttribute((const void*)k_buildt<NTH>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int iters = 400;
+  k_buildt<NTH><<<blocks, NTH, lds>>>(out, 4);
+  CK(hipDeviceSynchronize());
+  {
+    unsigned long long z[8] = {0};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(tqr::g_bt), z, sizeof(z)));
+  }
+  float ms;
+  CK(hipEventRecord(e0));
+  k_buildt<NTH><<<blocks, NTH, lds>>>(out, iters);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  printf("build_t+pack_t %3d threads: %7.2f us per group\n", NTH, ms * 1e3 / iters);
+  unsigned long long bt[8];
+  CK(hipMemcpyFromSymbol(bt, HIP_SYMBOL(tqr::g_bt), sizeof(bt)));
+  const double tot = (double)(bt[3] - bt[0]);
+  printf("   build_t phases (share of build_t, block 0): Gram %.0f%%, sum %.0f%%, back-subst %.0f%%\n",
+         100.0 * (bt[1] - bt[0]) / tot, 100.0 * (bt[2] - bt[1]) / tot, 100.0 * (bt[3] - bt[2]) / tot);
+  unsigned long long z[8] = {0};
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(tqr::g_bt), z, sizeof(z)));
+  return 0;
 }
 
 template <bool TS, int NTH>
@@ -53,7 +104,8 @@ int main() {
   for (int blocks : {1, p.multiProcessorCount}) {
     printf("-- %d workgroup(s)\n", blocks);
     if (run<true, 256>("TSQRT", out, blocks) || run<true, 512>("TSQRT", out, blocks) ||
-        run<false, 256>("GEQRT", out, blocks) || run<false, 512>("GEQRT", out, blocks))
+        run<false, 256>("GEQRT", out, blocks) || run<false, 512>("GEQRT", out, blocks) ||
+        run_bt<256>(out, blocks) || run_bt<512>(out, blocks))
       return 1;
   }
   return 0;
