@@ -49,3 +49,9 @@ for a0, a1 in zip(edges[:-1], edges[1:]):
     ov = np.clip(np.minimum(e, a1) - np.maximum(s, a0), 0, None).sum() / (a1 - a0)
     occ.append(ov)
 print("  " + " ".join(f"{o:5.0f}" for o in occ))
+# panel members of a few steps: start/end per member
+for kk in (0, 1, 16):
+    pm = np.where((k == kk) & ~chain)[0]
+    order = pm[np.argsort(I[pm, 1])]
+    rows = [f"{I[x, 1]}:{s[x] / 1e3:.2f}-{e[x] / 1e3:.2f}" for x in order[:: max(1, len(order) // 12)]]
+    print(f" step {kk} members (tile row: start-end ms): " + " ".join(rows))
