@@ -344,6 +344,10 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
   const double Tg = eg ? atof(eg) : 1.4, Te = 1.0;
   const char* el = getenv("TQR_LAZY");
   const double lazy = el ? atof(el) : 1.0;
+  // lookahead (TQR_LA, unit: chain elements): panel tasks and the lookahead column's chains are
+  // keyed this much earlier than their estimate (the critical path first)
+  const char* ela = getenv("TQR_LA");
+  const double la = ela ? atof(ela) : 0.0;
   // fin_elem[k][i][j] (strips move together in the estimate): finish of chain element (i,j,k)
   auto id3 = [&](int k, int i, int j) { return ((size_t)k * p + i) * q + j; };
   std::vector<double> fin((size_t)kmax * p * q, 0.0), pstart((size_t)kmax * p, 0.0);
@@ -354,11 +358,11 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
     // panel
     double ps = fin_prev(k, k, k);
     pstart[(size_t)k * p + k] = ps;
-    tl.push_back({ps, 0, Item{QRS, k, k, k}});
+    tl.push_back({ps - la, 0, Item{QRS, k, k, k}});
     for (int i = k + 1; i < p; ++i) {
       double st = std::max(fin_prev(k, i, k), pstart[(size_t)k * p + i - 1] + Tg);
       pstart[(size_t)k * p + i] = st;
-      tl.push_back({st, 0, Item{QRD, i, k, k}});
+      tl.push_back({st - la, 0, Item{QRD, i, k, k}});
     }
     // chains
     for (int j = k + 1; j < q; ++j) {
@@ -384,6 +388,7 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
         // column k+1 feeds the next panel and stays eager
         double key = seg_start[std::min<size_t>(e, seg_start.size() - 1)];
         if (lazy > 0 && j != k + 1 && i0 < p) key = std::max(key, pstart[(size_t)k * p + i0] + lazy * ng * Tg);
+        if (j == k + 1) key -= la;
         for (int s = 0; s < ns; ++s)
           tl.push_back({key, 1,
                         Item{T_CHAIN | (s << 8), i0 | (i1 << 16), j, k | (e << 16)}});

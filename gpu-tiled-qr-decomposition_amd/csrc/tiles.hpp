@@ -647,10 +647,7 @@ __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, 
   const bool wr = (lane & (SPAN - 1)) == 0;
   double* rb = red + (C & 1) * 128;
   if (wr && w < 4) rb[w * 32 + cr] = ws;  // rows live in waves 0-3
-  if (!TS && rt == rc) {
-#pragma unroll
-    for (int j = 0; j < NW; ++j) hrow[(C & 1) * 32 + j] = x[j];
-  }
+  // (GE: the head row reached hrow at the end of the previous step, off this barrier's path)
   __syncthreads();
   const double Dm = (rb[cr] + rb[32 + cr]) + (rb[64 + cr] + rb[96 + cr]);
   const double Hm = TS ? (cw < IB ? Hs[C * TP + cw] : 0.0) : hrow[(C & 1) * 32 + cr];
@@ -673,22 +670,28 @@ __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, 
     f[2 * h] = v2.x;
     f[2 * h + 1] = v2.y;
   }
-  if (tail) {
-    const double xc = x[0] * scale;
+  // branch-free update (a divergent tail/head-row branch made the wave holding the GE head row
+  // run both streams): tails x_j -= f_j (scale x_C), the GE head row x_j -= f_j (coefficient 1,
+  // the same rounding as a subtraction), all other rows coefficient 0 (x_j unchanged)
+  const bool hr = !TS && rt == rc;
+  const double xc = x[0] * scale;
+  const double cf = tail ? xc : (hr ? 1.0 : 0.0);
 #pragma unroll
-    for (int j = 1; j < NW; ++j) x[j] = fma(-f[j], xc, x[j]);
-    x[0] = xc;
-  } else if (!TS && rt == rc) {
-#pragma unroll
-    for (int j = 1; j < NW; ++j) x[j] -= f[j];
-    x[0] = x0 - f[0];
-  }
+  for (int j = 1; j < NW; ++j) x[j] = fma(-f[j], cf, x[j]);
+  x[0] = tail ? xc : (hr ? x0 - f[0] : x[0]);
   if (t == 0) tauv[C] = tau;
   // column C is final (V entry / R entry): out to the image, shift the window
   if (own) Vs[t * VP + g::pc(C)] = x[0];
 #pragma unroll
   for (int j = 0; j + 1 < NW; ++j) x[j] = x[j + 1];
   x[NW - 1] = 0.0;
+  // GE: the next step's head row (updated just now as a tail) goes to the other hrow buffer
+  // (every wave read this one's twin before passing this step's barrier)
+  if (!TS && C + 1 < Geo<B>::IB && rt == rc + 1) {
+    double2* hb = reinterpret_cast<double2*>(hrow + ((C + 1) & 1) * 32);
+#pragma unroll
+    for (int h = 0; h < NW / 2; ++h) hb[h] = make_double2(x[2 * h], x[2 * h + 1]);
+  }
 }
 
 // PERM: LDS row q of Vs holds tile row vimg_row(q) (the chain engine's paired row order), else
@@ -716,6 +719,10 @@ __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, 
   double x[IB];
 #pragma unroll
   for (int j = 0; j < IB; ++j) x[j] = own ? Vs[t * VP + g::pc(j)] : 0.0;
+  if (!TS && rt == c0) {  // head row of step 0 (later ones: end of the previous step)
+#pragma unroll
+    for (int j = 0; j < IB; ++j) hrow[j] = x[j];
+  }
   // reduce the live window only: all IB columns while more than IB/2 are live, then the half
   constexpr int HALF = IB == 32 ? 16 : IB;
 #pragma clang loop unroll(disable)
