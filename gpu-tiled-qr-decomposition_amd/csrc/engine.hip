@@ -344,10 +344,12 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
   const double Tg = eg ? atof(eg) : 1.4, Te = 1.0;
   const char* el = getenv("TQR_LAZY");
   const double lazy = el ? atof(el) : 1.0;
-  // lookahead (TQR_LA, unit: chain elements): panel tasks and the lookahead column's chains are
-  // keyed this much earlier than their estimate (the critical path first)
+  // lookahead (TQR_LA / TQR_LAC, unit: chain elements): panel tasks / the lookahead column's
+  // chains are keyed this much earlier than their estimate (the critical path first)
   const char* ela = getenv("TQR_LA");
   const double la = ela ? atof(ela) : 0.0;
+  const char* elac = getenv("TQR_LAC");  // lookahead column's chains (default: TQR_LA)
+  const double lac = elac ? atof(elac) : la;
   // fin_elem[k][i][j] (strips move together in the estimate): finish of chain element (i,j,k)
   auto id3 = [&](int k, int i, int j) { return ((size_t)k * p + i) * q + j; };
   std::vector<double> fin((size_t)kmax * p * q, 0.0), pstart((size_t)kmax * p, 0.0);
@@ -388,7 +390,7 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
         // column k+1 feeds the next panel and stays eager
         double key = seg_start[std::min<size_t>(e, seg_start.size() - 1)];
         if (lazy > 0 && j != k + 1 && i0 < p) key = std::max(key, pstart[(size_t)k * p + i0] + lazy * ng * Tg);
-        if (j == k + 1) key -= la;
+        if (j == k + 1) key -= lac;
         for (int s = 0; s < ns; ++s)
           tl.push_back({key, 1,
                         Item{T_CHAIN | (s << 8), i0 | (i1 << 16), j, k | (e << 16)}});
