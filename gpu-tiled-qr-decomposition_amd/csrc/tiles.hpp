@@ -639,8 +639,9 @@ __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, 
   const int rc = c0 + C;  // GE: tile row of the reflector head
   const bool tail = own && (TS || rt > rc);  // rt: the tile row this thread holds
   double pv[NW];
+  const double xm = tail ? x[0] : 0.0;  // one select, not one per product (GE: 64 v_cndmask)
 #pragma unroll
-  for (int j = 0; j < NW; ++j) pv[j] = tail ? x[0] * x[j] : 0.0;
+  for (int j = 0; j < NW; ++j) pv[j] = xm * x[j];
   const double ws = RS<NW>::run(pv, lane);
   const int cr = rs_col<NW>(lane);  // relative column of this lane's sum
   const int cw = C + cr;            // absolute column (>= IB: outside the panel, ignored)
