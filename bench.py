@@ -51,52 +51,104 @@ def update_flops(m, n, b):
     return f
 
 
-def cpu_baseline(sample_n=6144, b=256, threads=8):
+def _host_threads():
+    """Host cores available to this process (the GPU box exports OMP_NUM_THREADS = its CPU share;
+    os.cpu_count() there is the whole machine)."""
+    v = os.environ.get("OMP_NUM_THREADS")
+    if v and v.isdigit() and int(v) > 0:
+        return int(v)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_factor(m, n, b, threads):
+    """One full factorisation on the host: the reference's own host path (oracle/_ref, its
+    pthr_doTasks worker loop + gridscheduler.c) when built, else the oracle port. Returns
+    (seconds, kind)."""
     import ctypes
 
     import numpy as np
     P = ctypes.c_void_p
-    ref = os.path.join(REPO, "oracle", "_ref", "libref_f64_fix.so")
-    m = n = sample_n
     A = np.zeros((n, m), dtype=np.float64)
     F = np.zeros_like(A)
     T = np.zeros_like(A)
+    ref = os.path.join(REPO, "oracle", "_ref", "libref_f64_fix.so")
     if os.path.exists(ref):
         L = ctypes.CDLL(ref)
         L.ref_factor.restype = ctypes.c_double
         L.ref_randzo(A.ctypes.data_as(P), m, n, m, 5)
-        t = L.ref_factor(A.ctypes.data_as(P), F.ctypes.data_as(P), T.ctypes.data_as(P), m, n, b, m, threads)
-        kind = "reference"
-    else:
-        lib = os.path.join(REPO, "oracle", "liboracle.so")
-        L = ctypes.CDLL(lib)
-        L.oracle_randzo_d(A.ctypes.data_as(P), m, n, m, 5)
-        t0 = time.perf_counter()
-        L.oracle_factor_threads_d(A.ctypes.data_as(P), F.ctypes.data_as(P), T.ctypes.data_as(P), m, n, b, m, threads)
-        t = time.perf_counter() - t0
-        kind = "port"
-    cpu = "unknown"
-    try:
-        for ln in open("/proc/cpuinfo"):
-            if ln.startswith("model name"):
-                cpu = ln.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {"value": round(qr_flops(m, n) / t / 1e9, 3), "unit": "GFLOP/s", "cores": threads, "kind": kind,
-            "sample": f"{m}x{n} fp64 b={b} RANDZO seed 5, full factorisation, {threads} pthreads "
-                      f"(reference taskQRP_threads worker loop, -O2), {t:.2f} s on {cpu}"}
+        return L.ref_factor(A.ctypes.data_as(P), F.ctypes.data_as(P), T.ctypes.data_as(P), m, n, b, m, threads), "reference"
+    L = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
+    L.oracle_randzo_d(A.ctypes.data_as(P), m, n, m, 5)
+    t0 = time.perf_counter()
+    L.oracle_factor_threads_d(A.ctypes.data_as(P), F.ctypes.data_as(P), T.ctypes.data_as(P), m, n, b, m, threads)
+    return time.perf_counter() - t0, "port"
 
 
-def load_traffic(m, n, b):
-    """HBM bytes per trailing-update launch from the committed rocprofv3 PMC summary."""
+def cpu_baseline(sample_n=6144, b=256):
+    """the reference host path at 8 threads (qrdecomp.c:21) and at all host cores
+    this process may use. Timed in full: configs[1] (4096^2, b=128) and a 6144^2 b=256 sample of
+    the configs[2] workload; configs[2] itself (16384^2, ~2 min of CPU) is extrapolated from the
+    sample's rate (same tile size, same kernels), and says so."""
+    nproc = _host_threads()
+    legs = {}
+    kind = "reference"
+    for name, thr in (("threads_8", 8), ("threads_nproc", nproc)):
+        leg = {"threads": thr}
+        t2, kind = _cpu_factor(4096, 4096, 128, thr)
+        leg["c2_4096x4096_b128_s"] = round(t2, 3)
+        leg["c2_gflops"] = round(qr_flops(4096, 4096) / t2 / 1e9, 3)
+        ts, kind = _cpu_factor(sample_n, sample_n, b, thr)
+        rate = qr_flops(sample_n, sample_n) / ts
+        leg[f"sample_{sample_n}x{sample_n}_b{b}_s"] = round(ts, 3)
+        leg["sample_gflops"] = round(rate / 1e9, 3)
+        leg["c3_16384x16384_b256_s_extrapolated"] = round(qr_flops(16384, 16384) / rate, 1)
+        legs[name] = leg
+    t8 = legs["threads_8"]
+    return {"value": t8["sample_gflops"], "unit": "GFLOP/s", "cores": 8, "kind": kind,
+            "sample": f"{sample_n}x{sample_n} fp64 b={b} RANDZO seed 5, full factorisation, 8 pthreads "
+                      f"(reference taskQRP_threads worker loop, -O2) on {_cpu_model()}",
+            "config": "configs[1] 4096x4096 b=128 timed in full; configs[2] 16384x16384 b=256 extrapolated "
+                      f"from the {sample_n}^2 b={b} sample rate",
+            "extrapolated": True,
+            "threads_8": legs["threads_8"], "threads_nproc": legs["threads_nproc"]}
+
+
+def load_pmc(m, n, b, storage):
+    """The committed rocprofv3 PMC summary of the k_flow launch (tools/pmc_summary.py): HBM bytes
+    per launch, executed MFMA flops, MFMA-pipe utilisation. None where not measured."""
     path = os.path.join(REPO, "profiles", "pmc_summary.json")
+    key = f"{m}x{n}_b{b}" + ("_f32" if storage == "f32" else "")
     try:
-        d = json.load(open(path))
-        e = d.get(f"{m}x{n}_b{b}")
-        return e["update_hbm_bytes_per_launch"] if e else None
-    except (OSError, ValueError, KeyError):
+        return json.load(open(path)).get(key)
+    except (OSError, ValueError):
         return None
+
+
+def check_output(A0, A, m, n):
+    """Cheap correctness check of the final factorisation (outside the timed region): Q is
+    orthogonal, so every column of R has the norm of the same column of A."""
+    import torch
+    R = torch.triu(A.T.double()).T  # (n, m) storage: zero below the diagonal
+    na = torch.linalg.vector_norm(A0.double(), dim=1)
+    nr = torch.linalg.vector_norm(R[:, :m], dim=1)
+    rel = ((na - nr).abs() / na.clamp_min(1e-300)).max().item()
+    tol = 1e-10 if A.dtype == torch.float64 else 1e-4
+    if not rel <= tol:
+        raise RuntimeError(f"bench: factorisation check failed (column-norm error {rel:.3e} > {tol})")
+    return rel
 
 
 def main():
@@ -155,6 +207,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    plan.status(stream)  # the engine's error word (outside the timed region)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -170,8 +223,8 @@ def main():
         tt = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
-    if hasattr(plan, "status"):
-        plan.status(stream)
+    plan.status(stream)
+    ok_rel = check_output(A0, A, m, n) if world == 1 else None
     ms_step = el / args.steps * 1e3
     total_flops = qr_flops(m, n) * args.steps
     value = total_flops / el / 1e9
@@ -186,7 +239,8 @@ def main():
     uf = update_flops(m, n, b)
     # per GPU: its share of the update flops (1/N of the job at N > 1) over its launch time
     achieved = uf / world / (st["ms_update"] * 1e-3) / 1e12 if st["ms_update"] > 0 else None
-    traffic = load_traffic(m, n, b)
+    pmc = load_pmc(m, n, b, args.storage) if world == 1 else None
+    traffic = pmc.get("update_hbm_bytes_per_launch") if pmc else None
     roof = {
         "bound": "mfma",
         "kernel": "k_flow (persistent engine; TSMQR/UNMQR strips on v_mfma_f64_4x4x4_4b_f64)",
@@ -195,6 +249,9 @@ def main():
         "unit": "TFLOP/s",
         "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4) if achieved else None,
         "traffic": traffic,
+        "executed_flops": pmc.get("executed_mfma_flops") if pmc else None,
+        "mfma_util": round(pmc["mfma_util"], 4) if pmc and pmc.get("mfma_util") is not None else None,
+        "pmc_source": "profiles/pmc_summary.json (rocprofv3 --pmc, tools/pmc_traffic.sh)" if pmc else None,
         "launches": st["n_update"],
         "avg_launch_ms": round(st["ms_update"] / max(1, st["n_update"]), 4),
         "algorithmic_flops_per_launch": round(uf / max(1, st["n_update"])),
@@ -203,7 +260,7 @@ def main():
     }
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_sample, b)
+        cpu = cpu_baseline(args.cpu_sample, 256)
 
     cfg = 2 if (m, n) == (16384, 16384) else 3 if (m, n) == (65536, 16384) else 1 if (m, n) == (4096, 4096) else "custom"
     if args.storage == "f32":
@@ -227,6 +284,7 @@ def main():
                        f"{world} GPUs, tile-column cyclic, panel V/T forwarded over xGMI"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "check": {"column_norm_rel_err": ok_rel} if ok_rel is not None else None,
         }
         print(json.dumps(line))
     if dist:

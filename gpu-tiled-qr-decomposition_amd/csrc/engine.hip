@@ -314,7 +314,7 @@ static size_t lds_flow(int b) {
     case 128: d = flow_lds_doubles<128>(); break;
     case 256: d = flow_lds_doubles<256>(); break;
   }
-  return (size_t)d * sizeof(double) + 256;  // + task index, FST sums, sync-point verdicts, Rc view
+  return (size_t)d * sizeof(double) + 512;  // + task index, sync-point verdicts, Rc view, FST sums
 }
 static ffn resolve_flow(int b, int dtype) {
   ffn f = nullptr;
@@ -337,8 +337,14 @@ struct FlowPlan {
   bool est_order = false;
 };
 
-static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
+static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp) {
   const int kmax = std::min(p, q), ns = (b + FLOW_SW - 1) / FLOW_SW, ng = b / (b < 32 ? b : 32);
+  // segment length per chain: the lookahead column (j = k+1, the DAG's critical path: its chain
+  // elements feed the next panel's members) may use shorter segments (TQR_SEGLEN_LA), which
+  // pipeline consecutive elements on different workgroups at reflector-group granularity
+  const char* esl = getenv("TQR_SEGLEN_LA");
+  const int seglen_la = esl ? std::max(1, atoi(esl)) : seglen_;
+  auto seglen_of = [&](int k, int j) { return j == k + 1 ? seglen_la : seglen_; };
   // cost model (unit: one chain element): Tg = one panel group-step; tunable for experiments
   const char* eg = getenv("TQR_TG");
   const double Tg = eg ? atof(eg) : 1.4, Te = 1.0;
@@ -373,6 +379,7 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
       fin[id3(k, k, j)] = prev;
       std::vector<double> seg_start;
       seg_start.push_back(t0);
+      const int seglen = seglen_of(k, j);
       for (int i = k + 1; i < p; ++i) {
         double st = std::max({prev, fin_prev(k, i, j), pstart[(size_t)k * p + i] + Tg});
         if ((i - k - 1) % seglen == 0 && i > k + 1) seg_start.push_back(st);
@@ -406,7 +413,7 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
       if (ty == T_CHAIN) pos[std::make_tuple(T_CHAIN, it.k & 0xffff, it.m, (it.ts >> 8) & 0xff, it.k >> 16)] = x;
       else pos[std::make_tuple(0, it.l, it.k, 0, 0)] = x;
     }
-    auto seg_of = [&](int k, int i) { return (i - k - 1) / seglen; };
+    auto seg_of = [&](int k, int j, int i) { return (i - k - 1) / seglen_of(k, j); };
     for (int x = 0; x < (int)L.size(); ++x) {
       const Item& it = L[x];
       int ty = it.ts & 0xff;
@@ -415,16 +422,16 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
         int s = (it.ts >> 8) & 0xff, k = it.k & 0xffff, e = it.k >> 16, j = it.m, i0 = it.l & 0xffff, i1 = it.l >> 16;
         if (e > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k, j, s, e - 1)]);
         else deps.push_back(pos[std::make_tuple(0, k, k, 0, 0)]);
-        if (e == 0 && k > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, k))]);
+        if (e == 0 && k > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, j, k))]);
         for (int i = i0; i < i1; ++i) {
           deps.push_back(pos[std::make_tuple(0, i, k, 0, 0)]);
-          if (k > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, i))]);
+          if (k > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, j, i))]);
         }
       } else {
         int i = it.l, k = it.k;
         if (i > k) deps.push_back(pos[std::make_tuple(0, i - 1, k, 0, 0)]);
         if (k > 0)
-          for (int s = 0; s < ns; ++s) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, k, s, seg_of(k - 1, i))]);
+          for (int s = 0; s < ns; ++s) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, k, s, seg_of(k - 1, k, i))]);
       }
       for (int d : deps)
         if (d >= x) {
@@ -448,7 +455,7 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
       if (ty == T_CHAIN) idx[std::make_tuple(T_CHAIN, it.k & 0xffff, it.m, (it.ts >> 8) & 0xff, it.k >> 16)] = x;
       else idx[std::make_tuple(0, it.l, it.k, 0, 0)] = x;
     }
-    auto seg_of = [&](int k, int i) { return (i - k - 1) / seglen; };
+    auto seg_of = [&](int k, int j, int i) { return (i - k - 1) / seglen_of(k, j); };
     for (int x = 0; x < (int)tl.size(); ++x) {
       const Item& it = tl[x].it;
       int ty = it.ts & 0xff;
@@ -458,16 +465,16 @@ static void build_flow_plan(int p, int q, int b, int seglen, FlowPlan& fp) {
         int s = (it.ts >> 8) & 0xff, k = it.k & 0xffff, e = it.k >> 16, j = it.m, i0 = it.l & 0xffff, i1 = it.l >> 16;
         if (e > 0) bump(idx[std::make_tuple(T_CHAIN, k, j, s, e - 1)]);
         else bump(idx[std::make_tuple(0, k, k, 0, 0)]);
-        if (e == 0 && k > 0) bump(idx[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, k))]);
+        if (e == 0 && k > 0) bump(idx[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, j, k))]);
         for (int i = i0; i < i1; ++i) {
           bump(idx[std::make_tuple(0, i, k, 0, 0)]);
-          if (k > 0) bump(idx[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, i))]);
+          if (k > 0) bump(idx[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, j, i))]);
         }
       } else {
         int i = it.l, k = it.k;
         if (i > k) bump(idx[std::make_tuple(0, i - 1, k, 0, 0)]);
         if (k > 0)
-          for (int s = 0; s < ns; ++s) bump(idx[std::make_tuple(T_CHAIN, k - 1, k, s, seg_of(k - 1, i))]);
+          for (int s = 0; s < ns; ++s) bump(idx[std::make_tuple(T_CHAIN, k - 1, k, s, seg_of(k - 1, k, i))]);
       }
       tl[x].est = key;
     }
@@ -524,6 +531,10 @@ static int resolve(int b, int dtype, kfn* kp, kfn* ku, kfn* kt) {
 }
 
 static bool valid_b(int b) { return b == 16 || b == 32 || b == 64 || b == 128 || b == 256; }
+// The engine's buffer resources are based at a strip's or reflector group's first column and
+// address at most 32 columns with 32-bit byte offsets (tiles.hpp load_strip_pair, flow.hpp):
+// 32 * ldm * es must stay below 2^31 (ldm <= 8,388,607 rows fp64, 16,777,215 fp32).
+static bool valid_ld(long ld, size_t es) { return ld > 0 && (size_t)32 * (size_t)ld * es <= 0x7fffffffull; }
 // workspace slot sizes (doubles) of Geo<b>::TIMG / VIMG
 static size_t timg_doubles(int b) {
   const size_t ib = b < 32 ? b : 32;
@@ -582,6 +593,11 @@ struct tqr_plan {
   PeerBufs* d_peers = nullptr;
   double** d_peer_wk = nullptr;  // world x kmax opened peer workspace pointers
   std::vector<void*> opened;     // IPC-opened peer pointers
+  bool imported = false;         // tqr_dist_import succeeded (world > 1 may execute)
+  // executions of one plan share its counters and workspaces: they are serialised — a host
+  // mutex around each enqueue sequence, and every execute's stream waits for the previous one
+  std::mutex mu;
+  hipEvent_t evDone = nullptr;
 };
 
 #define HIPCHK(x)                                                                         \
@@ -626,6 +642,7 @@ static int check_device() {
   return TQR_OK;
 }
 
+static void close_opened(tqr_plan* pl);
 void tqr_plan_destroy(tqr_plan* pl) {
   if (!pl) return;
   if (pl->d_items_p) (void)hipFree(pl->d_items_p);
@@ -642,24 +659,32 @@ void tqr_plan_destroy(tqr_plan* pl) {
   if (pl->d_sync) (void)hipFree(pl->d_sync);
   if (pl->ev0) (void)hipEventDestroy(pl->ev0);
   if (pl->ev1) (void)hipEventDestroy(pl->ev1);
+  if (pl->evDone) (void)hipEventDestroy(pl->evDone);
   for (auto e : pl->prof_ev) (void)hipEventDestroy(e);
-  for (void* p : pl->opened) (void)hipIpcCloseMemHandle(p);
+  close_opened(pl);
   if (pl->d_peers) (void)hipFree(pl->d_peers);
   if (pl->d_peer_wk) (void)hipFree(pl->d_peer_wk);
   if (pl->d_rf) (void)hipFree(pl->d_rf);
   delete pl;
 }
 
-static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world);
-int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) { return plan_create(out, m, n, b, dtype, 0, 1); }
+static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world, int engine);
+int tqr_plan_create(tqr_plan** out, int m, int n, int b, int dtype) {
+  return plan_create(out, m, n, b, dtype, 0, 1, TQR_ENGINE_DEFAULT);
+}
+int tqr_plan_create_engine(tqr_plan** out, int m, int n, int b, int dtype, int engine) {
+  if (engine != TQR_ENGINE_DEFAULT && engine != TQR_ENGINE_WAVES && engine != TQR_ENGINE_FLOW) return TQR_EINVAL;
+  return plan_create(out, m, n, b, dtype, 0, 1, engine);
+}
 int tqr_dist_plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world) {
   if (world < 1 || rank < 0 || rank >= world) return TQR_EINVAL;
-  return plan_create(out, m, n, b, dtype, rank, world);
+  return plan_create(out, m, n, b, dtype, rank, world, TQR_ENGINE_FLOW);
 }
-static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world) {
+static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world, int engine) {
   if (!out) return TQR_EINVAL;
   *out = nullptr;
-  if (!valid_b(b) || m <= 0 || n <= 0 || m % b || n % b || (dtype != TQR_F32 && dtype != TQR_F64))
+  if (!valid_b(b) || m <= 0 || n <= 0 || m % b || n % b || (dtype != TQR_F32 && dtype != TQR_F64) ||
+      !valid_ld(m, dtype == TQR_F64 ? 8 : 4))
     return TQR_EINVAL;
   int st = check_device();
   if (st) return st;
@@ -695,8 +720,11 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
   tqr_sched_plan_free(&sp);
 
   int ib = b < 32 ? b : 32;
-  const char* eng = getenv("TQR_ENGINE");
-  pl->engine = (eng && strcmp(eng, "waves") == 0 && world == 1) ? 0 : 1;
+  if (engine == TQR_ENGINE_DEFAULT) {
+    const char* eng = getenv("TQR_ENGINE");
+    engine = (eng && strcmp(eng, "waves") == 0) ? TQR_ENGINE_WAVES : TQR_ENGINE_FLOW;
+  }
+  pl->engine = world > 1 ? TQR_ENGINE_FLOW : engine;  // the multi-GPU protocol lives in the flow engine
   size_t tw = pl->engine == 0 ? (size_t)pl->p * pl->kmax * (b / ib) * timg_doubles(b) * sizeof(double) : 8;
   if (hipMalloc(&pl->d_items_p, std::max<size_t>(1, ip.size()) * sizeof(Item)) != hipSuccess ||
       hipMalloc(&pl->d_items_u, std::max<size_t>(1, iu.size()) * sizeof(Item)) != hipSuccess ||
@@ -721,10 +749,14 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
   if (resolve(b, dtype, &pl->kp, &pl->ku, &kt) != TQR_OK) { tqr_plan_destroy(pl); return TQR_EHIP; }
   pl->ldsP = lds_panel(b);
   pl->ldsU = lds_update(b);
+  if (hipEventCreate(&pl->ev0) != hipSuccess || hipEventCreate(&pl->ev1) != hipSuccess ||
+      hipEventCreateWithFlags(&pl->evDone, hipEventDisableTiming) != hipSuccess) {
+    tqr_plan_destroy(pl); return TQR_EHIP;
+  }
   // persistent dataflow engine: task list, progress counters, panel workspaces, kernel
   pl->ns = (b + FLOW_SW - 1) / FLOW_SW;  // chain strips per tile
   pl->ng = b / ib;
-  {
+  if (pl->engine == TQR_ENGINE_FLOW) {
     FlowPlan fp;
     const char* sl = getenv("TQR_SEGLEN");
     build_flow_plan(pl->p, pl->q, b, sl ? std::max(1, atoi(sl)) : 8, fp);
@@ -769,9 +801,6 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     pl->grid = pr.multiProcessorCount;
     const char* gs = getenv("TQR_FLOW_GRID");
     if (gs) pl->grid = std::max(1, atoi(gs));
-    if (hipEventCreate(&pl->ev0) != hipSuccess || hipEventCreate(&pl->ev1) != hipSuccess) {
-      tqr_plan_destroy(pl); return TQR_EHIP;
-    }
   }
   *out = pl;
   return TQR_OK;
@@ -779,8 +808,8 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
 
 int tqr_plan_status(tqr_plan* pl, void* stream) {
   if (!pl) return TQR_EINVAL;
-  if (pl->engine != 1) return TQR_OK;
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  if (pl->engine != TQR_ENGINE_FLOW) return TQR_OK;  // wave engine: no in-kernel waits to time out
   int err = 0;
   HIPCHK(hipMemcpy(&err, pl->d_sync + 1, sizeof(int), hipMemcpyDeviceToHost));
   if (err) {
@@ -791,22 +820,66 @@ int tqr_plan_status(tqr_plan* pl, void* stream) {
 }
 
 // ---- multi-GPU ------------------------------------------------------------------------------
+// handle block: the PCI bus id of the exporting device (64 bytes), then the IPC handles of its
+// member flags and of its per-step panel workspaces
+static constexpr size_t kBusIdBytes = 64;
 size_t tqr_dist_handle_bytes(const tqr_plan* pl) {
-  return pl ? sizeof(hipIpcMemHandle_t) * (1 + (size_t)pl->kmax) : 0;
+  return pl ? kBusIdBytes + sizeof(hipIpcMemHandle_t) * (1 + (size_t)pl->kmax) : 0;
 }
 
 int tqr_dist_export(tqr_plan* pl, void* buf, size_t len) {
   if (!pl || pl->world < 2 || !buf || len < tqr_dist_handle_bytes(pl)) return TQR_EINVAL;
+  char bus[kBusIdBytes] = {0};
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  HIPCHK(hipDeviceGetPCIBusId(bus, (int)kBusIdBytes - 1, dev));
   std::vector<hipIpcMemHandle_t> h(1 + pl->kmax);
   HIPCHK(hipIpcGetMemHandle(&h[0], pl->d_rf));
   for (int k = 0; k < pl->kmax; ++k) HIPCHK(hipIpcGetMemHandle(&h[1 + k], pl->wk[k]));
-  memcpy(buf, h.data(), sizeof(hipIpcMemHandle_t) * h.size());
+  memcpy(buf, bus, kBusIdBytes);
+  memcpy((char*)buf + kBusIdBytes, h.data(), sizeof(hipIpcMemHandle_t) * h.size());
+  return TQR_OK;
+}
+
+static void close_opened(tqr_plan* pl) {
+  for (void* p : pl->opened) (void)hipIpcCloseMemHandle(p);
+  pl->opened.clear();
+}
+
+// Peer reachability of the device that exported `bus`: the same device (ranks sharing a GPU)
+// needs nothing; another device must be peer-accessible from this one (xGMI), and peer access
+// is enabled explicitly before any handle is opened — a missing link fails here, loudly,
+// instead of as a fault or a hang inside the persistent launch.
+static int enable_peer(int rank, int r, const char* bus) {
+  int me = 0, peer = -1;
+  HIPCHK(hipGetDevice(&me));
+  if (hipDeviceGetByPCIBusId(&peer, bus) != hipSuccess) {
+    (void)hipGetLastError();
+    // not visible in this process (e.g. HIP_VISIBLE_DEVICES): the IPC open decides
+    fprintf(stderr, "tqr: rank %d: rank %d's device %s is not visible here; relying on IPC peer mapping\n", rank, r, bus);
+    return TQR_OK;
+  }
+  if (peer == me) return TQR_OK;
+  int can = 0;
+  HIPCHK(hipDeviceCanAccessPeer(&can, me, peer));
+  if (!can) {
+    fprintf(stderr, "tqr: rank %d: device %d cannot access rank %d's device %d (%s): no peer path\n", rank, me, r, peer, bus);
+    return TQR_EHIP;
+  }
+  hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+  } else if (e != hipSuccess) {
+    fprintf(stderr, "tqr: rank %d: enabling peer access to device %d failed: %s\n", rank, peer, hipGetErrorString(e));
+    return TQR_EHIP;
+  }
   return TQR_OK;
 }
 
 int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
   const size_t hb = tqr_dist_handle_bytes(pl);
-  if (!pl || pl->world < 2 || !all || len < (size_t)pl->world * hb || !pl->opened.empty()) return TQR_EINVAL;
+  if (!pl || pl->world < 2 || !all || len < (size_t)pl->world * hb || pl->imported) return TQR_EINVAL;
+  close_opened(pl);  // a previous failed import
   std::vector<PeerBufs> pb(pl->world);
   std::vector<double*> pwk((size_t)pl->world * pl->kmax, nullptr);
   for (int r = 0; r < pl->world; ++r) {
@@ -816,12 +889,19 @@ int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
       pb[r] = PeerBufs{tab, pl->d_rf};
       continue;
     }
+    const char* blk = (const char*)all + (size_t)r * hb;
+    char bus[kBusIdBytes];
+    memcpy(bus, blk, kBusIdBytes);
+    bus[kBusIdBytes - 1] = 0;
+    int st = enable_peer(pl->rank, r, bus);
+    if (st) { close_opened(pl); return st; }
     std::vector<hipIpcMemHandle_t> h(1 + pl->kmax);
-    memcpy(h.data(), (const char*)all + (size_t)r * hb, hb);
-    void* p = nullptr;
+    memcpy(h.data(), blk + kBusIdBytes, hb - kBusIdBytes);
     for (int x = 0; x <= pl->kmax; ++x) {
+      void* p = nullptr;
       if (hipIpcOpenMemHandle(&p, h[x], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
         fprintf(stderr, "tqr: rank %d cannot open rank %d's workspace (IPC handle %d)\n", pl->rank, r, x);
+        close_opened(pl);
         return TQR_EHIP;
       }
       pl->opened.push_back(p);
@@ -830,14 +910,20 @@ int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
     }
     pb[r].Wk = tab;
   }
-  HIPCHK(hipMemcpy(pl->d_peer_wk, pwk.data(), sizeof(double*) * pwk.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(pl->d_peers, pb.data(), sizeof(PeerBufs) * pl->world, hipMemcpyHostToDevice));
+  if (hipMemcpy(pl->d_peer_wk, pwk.data(), sizeof(double*) * pwk.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(pl->d_peers, pb.data(), sizeof(PeerBufs) * pl->world, hipMemcpyHostToDevice) != hipSuccess) {
+    close_opened(pl);
+    return TQR_EHIP;
+  }
+  pl->imported = true;
   return TQR_OK;
 }
 
 int tqr_dist_reset(tqr_plan* pl, void* stream) {
   if (!pl || pl->world < 2) return TQR_EINVAL;
   hipStream_t cs = (hipStream_t)stream;
+  std::lock_guard<std::mutex> lk(pl->mu);
+  HIPCHK(hipStreamWaitEvent(cs, pl->evDone, 0));
   HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
   HIPCHK(hipMemsetAsync(pl->d_rf, 0, sizeof(int) * (size_t)pl->kmax * pl->p * pl->ng, cs));
   return TQR_OK;
@@ -863,6 +949,19 @@ int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, in
 }
 
 int tqr_flow_strip_width(void) { return FLOW_SW; }
+
+int tqr_flow_plan_export(int M, int N, int b, int seglen, int* items, int cap) {
+  if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1) return TQR_EINVAL;
+  FlowPlan fp;
+  build_flow_plan(M, N, b, seglen, fp);
+  const int n = (int)fp.items.size();
+  if (items)
+    for (int x = 0; x < n && x < cap; ++x) {
+      items[4 * x] = fp.items[x].ts; items[4 * x + 1] = fp.items[x].l;
+      items[4 * x + 2] = fp.items[x].m; items[4 * x + 3] = fp.items[x].k;
+    }
+  return n;
+}
 
 int tqr_flow_plan_check(int M, int N, int b, int seglen, int* ntasks, int* est_order) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1) return TQR_EINVAL;
@@ -897,9 +996,19 @@ int tqr_plan_stats(const tqr_plan* pl, int* nu, double* msu, int* np, double* ms
   return TQR_OK;
 }
 
+static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_t cs);
 int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream) {
-  if (!pl || !dA || !dtau || ldda < pl->m) return TQR_EINVAL;
+  if (!pl || !dA || !dtau || ldda < pl->m || !valid_ld(ldda, pl->es)) return TQR_EINVAL;
+  // a multi-GPU plan whose peers were never imported would dereference unset peer pointers
+  if (pl->world > 1 && !pl->imported) return TQR_EINVAL;
   hipStream_t cs = (hipStream_t)stream;
+  std::lock_guard<std::mutex> lk(pl->mu);
+  HIPCHK(hipStreamWaitEvent(cs, pl->evDone, 0));  // the previous execute of this plan (any stream)
+  int st = plan_execute(pl, dA, ldda, dtau, cs);
+  if (st == TQR_OK) HIPCHK(hipEventRecord(pl->evDone, cs));
+  return st;
+}
+static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_t cs) {
   if (pl->engine == 1) {
     if (!pl->kflow || !pl->d_flow || !pl->d_sync) return TQR_EINVAL;
     FlowArgs f;
@@ -984,16 +1093,16 @@ int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream)
 
 // ---- plan cache for the one-shot helpers -------------------------------------------------
 static std::mutex g_cache_mu;
-static std::map<std::tuple<int, int, int, int, int>, tqr_plan*> g_cache;
+static std::map<std::tuple<int, int, int, int, int, int>, tqr_plan*> g_cache;
 
-static int cached_plan(int m, int n, int b, int dtype, tqr_plan** out) {
+static int cached_plan(int m, int n, int b, int dtype, tqr_plan** out, int engine = TQR_ENGINE_DEFAULT) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return TQR_ENODEV;
   std::lock_guard<std::mutex> lk(g_cache_mu);
-  auto key = std::make_tuple(dev, m, n, b, dtype);
+  auto key = std::make_tuple(dev, m, n, b, dtype, engine);
   auto itc = g_cache.find(key);
   if (itc != g_cache.end()) { *out = itc->second; return TQR_OK; }
-  int st = tqr_plan_create(out, m, n, b, dtype);
+  int st = tqr_plan_create_engine(out, m, n, b, dtype, engine);
   if (st == TQR_OK) g_cache[key] = *out;
   return st;
 }
@@ -1011,10 +1120,10 @@ int tqr_sgeqrt_tiled(int m, int n, int b, float* dA, int ldda, float* dtau, void
 
 // Host-pointer factorisation: 2-D copies in, factorise, copies out, tau expanded to the
 // reference's m x n layout (column k*b of tau = compact column k).
-static int geqrt_host(void* A, void* tau, int m, int n, int ldm, int b, int dtype) {
+static int geqrt_host(void* A, void* tau, int m, int n, int ldm, int b, int dtype, int engine = TQR_ENGINE_DEFAULT) {
   if (!A || ldm < m || !valid_b(b) || m <= 0 || n <= 0 || m % b || n % b) return TQR_EINVAL;
   tqr_plan* pl;
-  int st = cached_plan(m, n, b, dtype, &pl);
+  int st = cached_plan(m, n, b, dtype, &pl, engine);
   if (st) return st;
   size_t es = dtype == TQR_F64 ? 8 : 4;
   void *dA = nullptr, *dT = nullptr;
@@ -1043,6 +1152,11 @@ static int geqrt_host(void* A, void* tau, int m, int n, int ldm, int b, int dtyp
 
 int tqr_dgeqrt_host(double* A, double* tau, int m, int n, int ldm, int b) { return geqrt_host(A, tau, m, n, ldm, b, TQR_F64); }
 int tqr_sgeqrt_host(float* A, float* tau, int m, int n, int ldm, int b) { return geqrt_host(A, tau, m, n, ldm, b, TQR_F32); }
+int tqr_geqrt_host_engine(int dtype, void* A, void* tau, int m, int n, int ldm, int b, int engine) {
+  if (dtype != TQR_F32 && dtype != TQR_F64) return TQR_EINVAL;
+  if (engine != TQR_ENGINE_DEFAULT && engine != TQR_ENGINE_WAVES && engine != TQR_ENGINE_FLOW) return TQR_EINVAL;
+  return geqrt_host(A, tau, m, n, ldm, b, dtype, engine);
+}
 
 int tqr_fill_randzo(int dtype, void* dA, int m, int n, int ldda, unsigned long long seed, void* stream) {
   if (!dA || ldda < m || m <= 0 || n <= 0) return TQR_EINVAL;
@@ -1177,6 +1291,74 @@ int tqr_tile_tsmqr(int dtype, const void* V, void* A, void* Bm, const void* tau,
   if (!st) st = tr.get(A, ldm, 0, 1);
   if (!st) st = tr.get(Bm, ldm, 1, 1);
   return st;
+}
+
+// Batched independent tile updates (the reference's testDAPP microbenchmark, gpucalc.cu:1687-1774,
+// generalised): nblocks copies of one tile (pair) updated by ONE launch of the update kernel.
+int tqr_tile_batch(int dtype, int type, int b, int nblocks, const void* V, int ldv, const void* tau,
+                   const void* blk, int ldb, void* out, int ldo, float* ms) {
+  if ((type != SAPP && type != DAPP) || nblocks <= 0 || !V || !tau || !blk || !valid_b(b) ||
+      (dtype != TQR_F32 && dtype != TQR_F64))
+    return TQR_EINVAL;
+  const int rows = type == DAPP ? 2 * b : b;  // rows of one block: [A; B] or C
+  if (ldv < b || ldb < rows || (out && ldo < rows)) return TQR_EINVAL;
+  int st = check_device();
+  if (st) return st;
+  kfn kp, ku, kt;
+  if ((st = resolve(b, dtype, &kp, &ku, &kt))) return st;
+  const size_t es = dtype == TQR_F64 ? 8 : 4;
+  const int mr = 2 * b, ng = b / (b < 32 ? b : 32), nstrips = (b + 63) / 64;
+  const size_t nc = (size_t)(1 + nblocks) * b;
+  void *dA = nullptr, *dtau = nullptr;
+  double* dT = nullptr;
+  Item* dit = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<Item> items;
+  items.push_back(type == DAPP ? Item{QRD, 1, 0, 0} : Item{QRS, 0, 0, 0});  // T factors of V
+  for (int j = 1; j <= nblocks; ++j)
+    for (int s = 0; s < nstrips; ++s) items.push_back(Item{type | (s << 8), type == DAPP ? 1 : 0, j, 0});
+  auto fin = [&](int code) {
+    if (dA) (void)hipFree(dA);
+    if (dtau) (void)hipFree(dtau);
+    if (dT) (void)hipFree(dT);
+    if (dit) (void)hipFree(dit);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    return code;
+  };
+  if (hipMalloc(&dA, es * mr * nc) != hipSuccess || hipMalloc(&dtau, es * mr) != hipSuccess ||
+      hipMalloc(&dT, sizeof(double) * 2 * ng * timg_doubles(b)) != hipSuccess ||
+      hipMalloc(&dit, sizeof(Item) * items.size()) != hipSuccess)
+    return fin(TQR_ENOMEM);
+  if (hipMemset(dA, 0, es * mr * nc) != hipSuccess || hipMemset(dtau, 0, es * mr) != hipSuccess ||
+      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+    return fin(TQR_EHIP);
+  const int vrow = type == DAPP ? b : 0;  // V: tile (1,0) (TSQRT V_B) or tile (0,0) (GEQRT V)
+  if (hipMemcpy2D((char*)dA + es * vrow, es * mr, V, es * ldv, es * b, b, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy((char*)dtau + es * vrow, tau, es * b, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dit, items.data(), sizeof(Item) * items.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return fin(TQR_EHIP);
+  for (int j = 1; j <= nblocks; ++j)
+    if (hipMemcpy2D((char*)dA + es * (size_t)j * b * mr, es * mr, blk, es * ldb, es * rows, b, hipMemcpyHostToDevice) != hipSuccess)
+      return fin(TQR_EHIP);
+  Args a;
+  a.A = dA; a.tau = dtau; a.Tw = dT; a.items = dit; a.ldm = mr; a.m = mr; a.p = 2; a.kmax = 1;
+  hipLaunchKernelGGL(kt, dim3(ng), dim3(NT), lds_build_t(b), 0, a);
+  if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return fin(TQR_EHIP);
+  a.items = dit + 1;
+  if (hipEventRecord(e0, 0) != hipSuccess) return fin(TQR_EHIP);
+  hipLaunchKernelGGL(ku, dim3((unsigned)(items.size() - 1)), dim3(NT), lds_update(b), 0, a);
+  if (hipGetLastError() != hipSuccess || hipEventRecord(e1, 0) != hipSuccess || hipEventSynchronize(e1) != hipSuccess)
+    return fin(TQR_EHIP);
+  float t = 0;
+  if (hipEventElapsedTime(&t, e0, e1) != hipSuccess) return fin(TQR_EHIP);
+  if (ms) *ms = t;
+  if (out)
+    for (int j = 1; j <= nblocks; ++j)
+      if (hipMemcpy2D((char*)out + es * (size_t)(j - 1) * b * ldo, es * ldo, (char*)dA + es * (size_t)j * b * mr, es * mr,
+                      es * rows, b, hipMemcpyDeviceToHost) != hipSuccess)
+        return fin(TQR_EHIP);
+  return fin(TQR_OK);
 }
 
 }  // extern "C"

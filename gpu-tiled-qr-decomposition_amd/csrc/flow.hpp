@@ -44,15 +44,19 @@ constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel memb
 // writeback + images, 11 panel build_t, 12 panel in-tile trailing update (+ its Rt publish),
 // 13 chain phase 2 (X += V W; 3 is then phase 1 Z alone), 14 chain next-head load, 15 chain
 // W = -T^T Z + head update, 16 panel trailing: strip/head loads, 17 panel trailing: stores
-// (12 is then the trailing's MFMA part + Rt publish).
-constexpr int FST_N = 18;
+// (12 is then the trailing's MFMA part + Rt publish), 18 / 19 chain Rc waits at an element's
+// start (lookahead column j = k+1 / other columns), 20 chain Rc waits inside a lookahead-column
+// element (0 is then the same for other columns), 21 / 22 chain drain of the wave's own memory
+// operations before the group's polls, groups > 0 / group 0 (stamps build only; at group 0 this
+// includes the element's strip loads, which the real kernel overlaps with phase 1).
+constexpr int FST_N = 23;
 #ifdef TQR_FLOW_STAMPS
 extern __device__ unsigned long long g_fst[];
 extern __device__ unsigned long long g_ttl[];  // per task: start, end (s_memrealtime), workgroup
 #define FST(c)                                                                            \
   do {                                                                                    \
     if (threadIdx.x == 0) {                                                               \
-      unsigned long long* l_ = reinterpret_cast<unsigned long long*>(sflag + 1);          \
+      unsigned long long* l_ = reinterpret_cast<unsigned long long*>(sflag + 63);         \
       const unsigned long long n_ = __builtin_amdgcn_s_memrealtime();                     \
       l_[1 + (c)] += n_ - l_[0];                                                          \
       l_[0] = n_;                                                                         \
@@ -245,7 +249,7 @@ struct DmaJob {
 // from a parity-alternating LDS slot (a slot is rewritten only after the next barrier).
 template <bool DRAIN>
 __device__ __forceinline__ bool sync_point(bool ok0, int* sflag, int& par) {
-  int* slot = sflag + 40 + par;  // LDS tail: [task][flag][FST sums 2..25][..][verdicts 41,42][..][Rc view 49..]
+  int* slot = sflag + 40 + par;  // LDS tail (ints from the task word): [task][flag][..][verdicts 41,42][..][Rc view 49..][..][FST sums 64..]
   par ^= 1;
   if (threadIdx.x == 0) *slot = ok0 ? 1 : 0;
   if (DRAIN) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -388,13 +392,13 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       FST(1);
     }
     {  // the group's B x IB block, row pairs as 16-B sc1 buffer loads (GEQRT: rows above c0 zero)
-      const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt);
+      const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt + (size_t)c0 * ldm);  // offsets span IB columns
       const int rlo = qrs ? c0 : 0;
 #pragma unroll 4
       for (int idx = t; idx < B * IB / 2; idx += FLOW_NT) {
         const int r = 2 * (idx % (B / 2)), c = idx / (B / 2);
         double v0 = 0.0, v1 = 0.0;
-        if (r >= rlo) ld_pair<S>(rs, (unsigned)(((size_t)(c0 + c) * ldm + r) * sizeof(S)), v0, v1);
+        if (r >= rlo) ld_pair<S>(rs, (unsigned)(((size_t)c * ldm + r) * sizeof(S)), v0, v1);
         Vs[vimg_inv(r) * VP + G::pc(c)] = v0;
         Vs[vimg_inv(r + 1) * VP + G::pc(c)] = v1;
       }
@@ -409,17 +413,19 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     FST(10);
     // Vs holds the panel rows in the chains' paired order (LDS row q = tile row vimg_row(q)): the
     // V image is then a verbatim copy and the trailing update moves 16-B row pairs
+#ifndef TQR_DIAG_NOPFACT  // what-if: no panel factorisation (results wrong)
     if (qrs) panel_factor<B, false, true>(Vs, Hs, tauv, scratch, c0);
     else panel_factor<B, true, true>(Vs, Hs, tauv, scratch, c0);
+#endif
     FST(5);
     {  // write-back of the factored block (R / V), row pairs as 16-B write-through stores
-      const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt);
+      const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt + (size_t)c0 * ldm);
       const int rlo = qrs ? c0 : 0;
 #pragma unroll 4
       for (int idx = t; idx < B * IB / 2; idx += FLOW_NT) {
         const int r = 2 * (idx % (B / 2)), c = idx / (B / 2);
         if (r >= rlo)
-          st_pair<S>(rs, (unsigned)(((size_t)(c0 + c) * ldm + r) * sizeof(S)), Vs[vimg_inv(r) * VP + G::pc(c)],
+          st_pair<S>(rs, (unsigned)(((size_t)c * ldm + r) * sizeof(S)), Vs[vimg_inv(r) * VP + G::pc(c)],
                      Vs[vimg_inv(r + 1) * VP + G::pc(c)]);
       }
     }
@@ -439,7 +445,9 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       __syncthreads();
     }
     FST(10);
+#ifndef TQR_DIAG_NOBT  // what-if: no T formation (results wrong)
     build_t<B>(Vs, tauv, Gs, Ts, Gp, 0);  // (permuted rows: the GE zero rows are not a prefix)
+#endif
     // packed T (the Gram buffer is free now): the trailing update's and the chains' T operand
     double* Tp = Gs;
     pack_t<B, FLOW_NT>(Ts, Tp);
@@ -467,12 +475,16 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     // neither loaded nor stored (finished R rows, which the next member's trailing may be
     // updating meanwhile); the head resource is empty for GEQRT (loads 0, stores dropped) —
     // see flow_chain's UNMQR element.
-    const __amdgpu_buffer_rsrc_t rsH = head_rsrc(Rt, !qrs);
     const int h0 = qrs ? c0 / 8 : 0;
+#ifdef TQR_DIAG_NOPTRAIL  // what-if: no in-tile trailing update (results wrong)
+    for (int s = nstr; s < nstr; s += FLOW_NT / 64) {
+#else
     for (int s = w; s < nstr; s += FLOW_NT / 64) {
+#endif
       asm volatile("" ::: "memory");
       const int col = c0 + IB + 16 * s;
-      const unsigned so = head_off<B, S>(ldm, c0, col);  // head row c0 + x, column col + lane's
+      const __amdgpu_buffer_rsrc_t rsH = head_rsrc(Rt + (size_t)col * ldm, !qrs);
+      const unsigned so = head_off<B, S>(ldm, c0);  // head row c0 + x, column col + lane's
       load_strip_pair<B, S>(X, Bt, ldm, col, h0);
       load_head_buf<B, S, 16>(H, rsH, so);
 #ifdef TQR_FLOW_STAMPS
@@ -597,7 +609,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         FST(8);
         if (ok && !dma_next) ok = ready(i, 0);
       }
-      FST(0);
+      FST(j == k + 1 ? 18 : 19);  // Rc wait at element start (lookahead column / other)
       if (!sync_point<false>(ok, sflag, par)) return;
     }
     FST(7);
@@ -616,8 +628,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     // are exactly the GE update (the zero rows add exact zeros) — one MFMA stream for both
     // element types keeps the register allocation of the hot TSMQR path clean (a separate GE
     // variant with ks0-skipping cost the TSMQR phase 2 its operand prefetch), for ~1 % extra flops.
-    const __amdgpu_buffer_rsrc_t hrs = head_rsrc(At, ts);  // UNMQR: empty resource, head = 0
-    const unsigned hoff = head_off<B, S>(ldm, 0, col);
+    const __amdgpu_buffer_rsrc_t hrs = head_rsrc(At + (size_t)col * ldm, ts);  // UNMQR: empty resource, head = 0
+    const unsigned hoff = head_off<B, S>(ldm, 0);
     if (FLOW_PF && active) load_head_buf<B, S, 16>(H, hrs, hoff);
     FST(4);
     const int inext = (i == k) ? i0 : i + 1;
@@ -628,6 +640,11 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     for (int g = 0; g < NG; ++g) {
       {
         bool ok = true;
+#ifdef TQR_FLOW_STAMPS
+        // (diagnostic) separate this wave's own memory drain from the dependency polls below
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        FST(g == 0 ? 22 : 21);
+#endif
         if (t == 0) {
           // first element of a later segment: head rows of group g+1 (prefetched below) final?
           if (i == ifirst && seg > 0 && g + 1 < NG) ok = spin_ge(&acg[g + 1], seg, err);
@@ -636,7 +653,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
             else if (has_next) ok = ready(inext, 0);
           }
         }
-        FST(0);
+        FST(j == k + 1 ? 20 : 0);  // Rc wait inside an element (lookahead column / other)
         // group 0: the strip / head loads of this element may still be in flight
         constexpr int NX = G::NKS / 2 + (FLOW_PF ? G::NRI : 0);
         if (!(g == 0 ? sync_point_first<NX>(ok, sflag, par, active) : sync_point<true>(ok, sflag, par)))
@@ -731,7 +748,7 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
   int* s_flag = s_task + 1;
 #ifdef TQR_FLOW_STAMPS
   if (threadIdx.x == 0) {
-    unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 2);
+    unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 64);
     l_[0] = __builtin_amdgcn_s_memrealtime();
     for (int c = 0; c < FST_N; ++c) l_[1 + c] = 0;
   }
@@ -771,7 +788,7 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
 #ifdef TQR_FLOW_STAMPS
   FST(6);
   if (threadIdx.x == 0) {
-    unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 2);
+    unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 64);
     for (int c = 0; c < FST_N; ++c) g_fst[blockIdx.x * FST_N + c] = l_[1 + c];
   }
 #endif

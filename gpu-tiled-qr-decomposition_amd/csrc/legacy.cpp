@@ -55,35 +55,38 @@ void cudaQRTask_d(double* mat, int m, int n, int ldm, int maxblocks) {
   if (st) die("cudaQRTask_d", st);
   printf("GPU: %5.3f ms\n", now_ms() - t0);
 }
-void cudaQRFull(float* mat, int m, int n) { cudaQRTask(mat, m, n, m, 0); }
+// The reference declares cudaQRFull (gpucalc.h:4) but only sketches it (gpucalc.cu:1801-1877,
+// commented out): a host-scheduled, level-synchronous factorisation with b = 32 tiles whose tile
+// tasks go round-robin onto NUMSTREAMS = 128 streams. Here it is the wave engine: the host
+// scheduler's BFS waves of the same DAG, each wave one batched panel launch and one batched
+// update launch on two HIP streams joined by events (tqr.h TQR_ENGINE_WAVES). ldm = m, in place,
+// tau discarded (as cudaQRTask).
+void cudaQRFull(float* mat, int m, int n) {
+  double t0 = now_ms();
+  int st = tqr_geqrt_host_engine(TQR_F32, mat, nullptr, m, n, m, 32, TQR_ENGINE_WAVES);
+  if (st) die("cudaQRFull", st);
+  printf("GPU: %5.3f ms\n", now_ms() - t0);
+}
 
-// TSMQR throughput hook (gpucalc.cu:1706-1774): timings[r] = ms of r-th batch of `nblocks`
-// independent b = 32 TSMQR tile updates (here: one 64 x (32*nblocks) fp32 panel factorised
-// down to its trailing update, timed with HIP events).
+// TSMQR throughput hook with the reference's semantics (gpucalc.cu:1706-1774): for each of the
+// n repetitions, srand(5), one 64 x 32 fp32 block and 32 taus drawn as ((rand() % 101) - 50) / 50,
+// `nblocks` independent DAPP (b = 32) updates of copies of that block — V = its rows 32..63, the
+// pair [A; B] = the block itself — in one launch; timings[t] = launch ms x nblocks, as the
+// reference reports it. (The reference's kernel addresses A at column blockIdx.x instead of block
+// column blockIdx.x, so its blocks overlap; here every block is its own copy.)
 void testDAPP(float* timings, int n, int nblocks) {
   if (!timings || n <= 0 || nblocks <= 0) return;
-  const int b = 32, m = 2 * b, cols = b * (nblocks + 1);
-  float* dA = nullptr;
-  float* dT = nullptr;
-  if (hipMalloc(&dA, sizeof(float) * (size_t)m * cols) != hipSuccess || hipMalloc(&dT, sizeof(float) * m * 2) != hipSuccess)
-    die("testDAPP", TQR_ENOMEM);
-  hipEvent_t e0, e1;
-  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) die("testDAPP", TQR_EHIP);
-  for (int r = 0; r < n; ++r) {
-    int st = tqr_fill_randzo(TQR_F32, dA, m, cols, m, 5 + r, nullptr);
-    if (!st && hipEventRecord(e0, nullptr) != hipSuccess) st = TQR_EHIP;
-    if (!st) st = tqr_sgeqrt_tiled(m, cols, b, dA, m, dT, nullptr);
-    if (!st && hipEventRecord(e1, nullptr) != hipSuccess) st = TQR_EHIP;
-    if (!st && hipEventSynchronize(e1) != hipSuccess) st = TQR_EHIP;
-    if (st) die("testDAPP", st);
+  const int b = 32;
+  float blk[64 * 32], tau[32];
+  for (int t = 0; t < n; ++t) {
+    srand(5);
+    for (int i = 0; i < 64 * 32; ++i) blk[i] = ((float)(rand() % 101) - 50.0f) / 50.0f;
+    for (int i = 0; i < 32; ++i) tau[i] = ((float)(rand() % 101) - 50.0f) / 50.0f;
     float ms = 0;
-    (void)hipEventElapsedTime(&ms, e0, e1);
-    timings[r] = ms;
+    int st = tqr_tile_batch(TQR_F32, DAPP, b, nblocks, blk + 32, 64, tau, blk, 64, nullptr, 0, &ms);
+    if (st) die("testDAPP", st);
+    timings[t] = ms * nblocks;
   }
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  (void)hipFree(dA);
-  (void)hipFree(dT);
 }
 
 // One TSMQR on a 64 x 64 fp32 matrix, as the reference's doCUDADAPP (gpucalc.cu:1776-1799):

@@ -320,10 +320,12 @@ __device__ __forceinline__ int vimg_row(int q) { return 8 * (q >> 3) + 2 * (q & 
 __device__ __forceinline__ int vimg_inv(int r) { return 8 * (r >> 3) + 4 * (r & 1) + ((r >> 1) & 3); }
 // h0: 8-row blocks above it are neither loaded (zero) nor stored (the GEQRT panel's finished
 // R rows, which other members' trailing updates may be writing meanwhile)
+// The resource is based at the strip's first column (wave-uniform), so the 32-bit offsets span
+// 16 columns only: ldm * sizeof(S) * 16 < 2^31 (checked by tqr_plan_create / execute).
 template <int B, typename S>
 __device__ __forceinline__ void load_strip_pair(double (&X)[Geo<B>::NKS], S* tile, size_t ldm, int col0, int h0 = 0) {
-  const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
-  __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile);
+  const int lane = threadIdx.x & 63, x = lane >> 4, c = lane & 15;
+  __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile + (size_t)col0 * ldm);
   const unsigned base = (unsigned)(((size_t)c * ldm + 2 * x) * sizeof(S));
   // per-access displacement in the scalar offset (one VGPR offset for the whole strip: an
   // unsigned voffset + constant cannot be folded into the immediate field without a no-wrap proof)
@@ -348,8 +350,8 @@ __device__ __forceinline__ void load_strip_pair(double (&X)[Geo<B>::NKS], S* til
 template <int B, typename S>
 __device__ __forceinline__ void store_strip_pair(const double (&X)[Geo<B>::NKS], S* tile, size_t ldm, int col0,
                                                  int h0 = 0) {
-  const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
-  __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile);
+  const int lane = threadIdx.x & 63, x = lane >> 4, c = lane & 15;
+  __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile + (size_t)col0 * ldm);
   const unsigned base = (unsigned)(((size_t)c * ldm + 2 * x) * sizeof(S));
 #pragma unroll
   for (int h = 0; h < Geo<B>::NKS / 2; ++h) {
@@ -377,9 +379,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t head_rsrc(const void* p, bool 
   const int n = __builtin_amdgcn_readfirstlane(on ? 0x7fffffff : 0);
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, n, 0x00020000);
 }
+// byte offset of (row r0 + x, column 4blk + y) relative to a resource based at the strip's
+// first column (head_rsrc(tile + col0 * ldm, ...))
 template <int B, typename S>
-__device__ __forceinline__ unsigned head_off(size_t ldm, int r0, int col0) {
-  const int lane = threadIdx.x & 63, x = lane >> 4, c = col0 + (lane & 15);
+__device__ __forceinline__ unsigned head_off(size_t ldm, int r0) {
+  const int lane = threadIdx.x & 63, x = lane >> 4, c = lane & 15;
   return (unsigned)(((size_t)c * ldm + r0 + x) * sizeof(S));
 }
 template <int B, typename S, int AUX>

@@ -159,6 +159,10 @@ class TiledQR:
         ldda = ldda or self.m
         check(lib().tqr_plan_execute(self.h, _ptr(A), ldda, _ptr(tau), _P(stream or 0)), "tqr_plan_execute")
 
+    def status(self, stream=None):
+        """Synchronise `stream` and raise if the engine reported an error (tqr_plan_status)."""
+        check(lib().tqr_plan_status(self.h, _P(stream or 0)), "tqr_plan_status")
+
     def set_profile(self, on=True):
         check(lib().tqr_plan_set_profile(self.h, int(on)))
 
@@ -227,9 +231,6 @@ class DistTiledQR(TiledQR):
             torch.cuda.synchronize()
             dist.barrier(group=self.group)
         check(lib().tqr_plan_execute(self.h, _ptr(A), ldda, _ptr(tau), _P(stream or 0)), "tqr_plan_execute")
-
-    def status(self, stream=None):
-        check(lib().tqr_plan_status(self.h, _P(stream or 0)), "tqr_plan_status")
 
 
 def dist_plan_check(M, N, b, rank, world, seglen=8):

@@ -11,9 +11,15 @@
  *     is wrong for m < n, gpucalc.cu:1546-1559); `maxblocks` is accepted and ignored (the
  *     HIP engine sizes its own launches); no device reset. Errors are printed to stderr and
  *     abort the process (no silent CPU fallback).
- *   * cudaQRFull: declared but never defined in the reference (gpucalc.cu:1801-1877 is
- *     commented out); here it is the same factorisation with ldm = m.
- *   * testDAPP / doCUDADAPP: the reference's TSMQR benchmark hooks (gpucalc.cu:1706, 1776).
+ *   * cudaQRFull: declared but never defined in the reference (gpucalc.cu:1801-1877 is a
+ *     commented-out sketch of a host-scheduled, level-synchronous, multi-stream factorisation);
+ *     here it is exactly that, natively: the wave engine (tqr.h TQR_ENGINE_WAVES) — the host
+ *     scheduler's BFS waves of the DAG, two batched launches per wave on two HIP streams. b = 32,
+ *     ldm = m, in place, tau discarded, prints "GPU: x ms".
+ *   * testDAPP (gpucalc.cu:1706): the reference's TSMQR benchmark — per repetition, srand(5), one
+ *     64 x 32 block and 32 taus of ((rand() % 101) - 50) / 50, `nblocks` independent b = 32 DAPPs
+ *     on copies of it in one launch, timings[t] = ms x nblocks (tqr.h tqr_tile_batch).
+ *   * doCUDADAPP (gpucalc.cu:1776): one DAPP on a 64 x 64 matrix, taus = its first 32 entries.
  */
 #ifndef GPUCOMP_H
 #define GPUCOMP_H

@@ -8,7 +8,9 @@
  *     (reference qrdecomp.c:522-523, 683-684);
  *   * Householder conventions of qrdecomp.c:1201-1272 (sign(0)=+1, v0=1, tau=2/v'v, tau=2
  *     for length-1 and zero columns).
- * The tile size b must divide m and n; b in {16, 32, 64, 128, 256}.
+ * The tile size b must divide m and n; b in {16, 32, 64, 128, 256}. The leading dimension is
+ * bounded by the engine's 32-bit buffer offsets: 32 * ldm * sizeof(element) < 2^31, i.e.
+ * ldm <= 8,388,607 (fp64) / 16,777,215 (fp32); larger values return TQR_EINVAL.
  *
  * tau, device API: "compact" m x kmax column-major array (kmax = min(m,n)/b), column k holds
  * the b*(p-k) taus of panel k in rows k*b .. m-1 — exactly column k*b of the reference's
@@ -43,11 +45,26 @@ typedef struct tqr_plan tqr_plan;
 /* Plan a factorisation of an m x n matrix of `dtype` with tile size b on the current HIP
  * device. */
 int tqr_plan_create(tqr_plan** plan, int m, int n, int b, int dtype);
+/* Execution engines (both compute the same factorisation, bit for bit per tile operation):
+ *   TQR_ENGINE_FLOW  — one persistent dataflow launch: workgroups pull GEQRT/TSQRT panel tasks
+ *                      and fused UNMQR/TSMQR column chains from a static topological list and
+ *                      synchronise through progress counters (default);
+ *   TQR_ENGINE_WAVES — the host scheduler's BFS waves of the reference DAG, two batched launches
+ *                      per wave (panel tasks, update strips) on two HIP streams joined by events:
+ *                      the level-synchronous multi-stream form of the reference's cudaQRFull
+ *                      sketch (src/gpucalc.cu:1801-1877).
+ * TQR_ENGINE_DEFAULT = FLOW unless the environment sets TQR_ENGINE=waves. */
+enum tqr_engine { TQR_ENGINE_DEFAULT = -1, TQR_ENGINE_WAVES = 0, TQR_ENGINE_FLOW = 1 };
+int tqr_plan_create_engine(tqr_plan** plan, int m, int n, int b, int dtype, int engine);
 void tqr_plan_destroy(tqr_plan* plan);
 
 /* Factorise device matrix dA (ldda >= m) in place; dtau_compact is device memory of
  * m * kmax elements of the same dtype. `stream` is a hipStream_t (NULL = default stream).
- * Stream-ordered: returns once all work is enqueued. */
+ * Stream-ordered: returns once all work is enqueued.
+ * A plan owns one set of progress counters and panel workspaces, so its executions are
+ * serialised: calls from several host threads are mutually excluded while they enqueue, and
+ * each execute's stream first waits for the plan's previous execute (whatever its stream). Two
+ * executes of one plan never overlap on the GPU; use one plan per concurrent factorisation. */
 int tqr_plan_execute(tqr_plan* plan, void* dA, int ldda, void* dtau_compact, void* stream);
 
 /* Synchronise `stream` and report whether the last execute completed (the persistent engine
@@ -64,6 +81,10 @@ int tqr_flow_plan_check(int M, int N, int b, int seglen, int* ntasks, int* est_o
 /* Columns of one chain strip of the persistent engine (a tile column is split into
  * ceil(b / width) strips; one workgroup updates one strip). */
 int tqr_flow_strip_width(void);
+/* Host-only: the persistent engine's task list for an M x N tile grid, 4 ints per task
+ * {type | strip << 8, l, m, k} (chains: type 4, l = i0 | i1 << 16, k = step | segment << 16);
+ * returns the number of tasks (writes at most `cap`). */
+int tqr_flow_plan_export(int M, int N, int b, int seglen, int* items, int cap);
 
 /* Per-launch statistics of the last execute (filled when the plan was created with
  * tqr_plan_set_profile(plan, 1)): number of kernel launches and the summed device time of
@@ -96,13 +117,16 @@ int tqr_dist_owner(const tqr_plan* plan, int tile_col);
 int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd);
 
 /* ---- one-shot helpers ------------------------------------------------------------------ */
-/* Device pointers, stream-ordered; plan cached per (m,n,b,dtype). */
+/* Device pointers, stream-ordered; plan cached per (device,m,n,b,dtype) and shared by all
+ * callers — concurrent calls with the same shape are serialised on the GPU (see execute). */
 int tqr_dgeqrt_tiled(int m, int n, int b, double* dA, int ldda, double* dtau_compact, void* stream);
 int tqr_sgeqrt_tiled(int m, int n, int b, float* dA, int ldda, float* dtau_compact, void* stream);
 
 /* Host pointers, blocking: A in place; tau = the reference's m x n tau matrix (ldm). */
 int tqr_dgeqrt_host(double* A, double* tau, int m, int n, int ldm, int b);
 int tqr_sgeqrt_host(float* A, float* tau, int m, int n, int ldm, int b);
+/* the same with an explicit engine (tqr_engine) and dtype */
+int tqr_geqrt_host_engine(int dtype, void* A, void* tau, int m, int n, int ldm, int b, int engine);
 
 /* Host pointers, single tile tasks on the GPU (the reference's per-tile kernels; used by
  * qrdecomp.h's SGEQRF/SLARFT/STSQRF/SSSRFT and by the per-tile parity tests). Tile pointers
@@ -112,6 +136,16 @@ int tqr_tile_geqrt(int dtype, void* blk, void* tau, int b, int ldm);
 int tqr_tile_unmqr(int dtype, void* C, const void* V, const void* tau, int b, int ldm);
 int tqr_tile_tsqrt(int dtype, void* A, void* B, void* tau, int b, int ldm);
 int tqr_tile_tsmqr(int dtype, const void* V, void* A, void* B, const void* tau, int b, int ldm);
+
+/* Batched independent tile updates in ONE launch of the update kernel (the reference's testDAPP
+ * microbenchmark, src/gpucalc.cu:1687-1774, generalised to UNMQR and any b): `nblocks` copies of
+ * the host block `blk` are each updated with the same reflectors.
+ *   type DAPP (TSMQR): V = b x b dense TSQRT V_B (ldv), tau = its b taus, blk = 2b x b [A; B] (ldb);
+ *   type SAPP (UNMQR): V = b x b GEQRT tile (unit-lower V below the diagonal), blk = b x b C.
+ * *ms = device time of the update launch (HIP events); out (optional) receives the nblocks
+ * results, block j at out + j*b*ldo. */
+int tqr_tile_batch(int dtype, int type, int b, int nblocks, const void* V, int ldv, const void* tau,
+                   const void* blk, int ldb, void* out, int ldo, float* ms);
 
 /* Device-side synthetic input with the reference's RANDZO distribution
  * ((r mod 201) - 100)/100 (qrdecomp.c:1383), from a counter-based hash of (seed, i, j). */

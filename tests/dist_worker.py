@@ -5,7 +5,12 @@ Every rank factorises the same RANDZO matrix with the tile-column partitioned en
 owned tile columns and taus of all ranks are gathered to rank 0 (gloo, host tensors) and
 compared with the single-GPU result: the per-tile operation sequence is identical, so the
 results must agree bit for bit. Runs the factorisation twice (counter reset / re-launch path).
-Prints one JSON line on rank 0. Usage: dist_worker.py m n b f64|f32 [device]
+Prints one JSON line on rank 0. Usage: dist_worker.py m n b f64|f32 [device] [gather|checksum]
+
+mode "checksum" (BASELINE-size shapes, e.g. 65536 x 16384): instead of gathering the matrix,
+every rank reduces each owned tile column (and tau column) on the device to two wrapping int64
+sums of the raw bit patterns (plain and position-weighted) and only these are gathered —
+bit-identical results give identical checksums.
 """
 import json
 import os
@@ -20,10 +25,21 @@ sys.path.insert(0, os.path.join(os.path.dirname(HERE), "gpu-tiled-qr-decompositi
 import tqr  # noqa: E402
 
 
+def checksums(blocks):
+    """(plain, position-weighted) wrapping int64 sums of each block's raw bits, on the device."""
+    out = []
+    for x in blocks:
+        v = x.contiguous().view(torch.int64 if x.dtype == torch.float64 else torch.int32).to(torch.int64).flatten()
+        w = torch.arange(1, v.numel() + 1, device=v.device, dtype=torch.int64)
+        out.append((int(v.sum().item()), int((v * w).sum().item())))
+    return out
+
+
 def main():
     m, n, b = (int(x) for x in sys.argv[1:4])
     dt = torch.float64 if sys.argv[4] == "f64" else torch.float32
     dev = int(sys.argv[5]) if len(sys.argv) > 5 else int(os.environ.get("LOCAL_RANK", "0"))
+    mode = sys.argv[6] if len(sys.argv) > 6 else "gather"
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -50,6 +66,32 @@ def main():
         plan.status()
         say(f"run {rep}: done")
         own = [j for j in range(q) if plan.owns(j)]
+        if mode == "checksum":
+            own_tau = [k for k in range(kmax) if plan.owns(k)]
+            mine = dict(zip(own, checksums([A[j * b:(j + 1) * b] for j in own])))
+            mine_tau = dict(zip(own_tau, checksums([tau[k] for k in own_tau])))
+            del A, tau
+            allcs = [None] * world
+            dist.all_gather_object(allcs, (mine, mine_tau))
+            say(f"run {rep}: checksums gathered")
+            if rank == 0:
+                ref = tqr.TiledQR(m, n, b, dt)
+                R = A0.clone()
+                rtau = torch.zeros((kmax, m), dtype=dt, device="cuda")
+                ref.execute(R, rtau)
+                ref.status()
+                rc = checksums([R[j * b:(j + 1) * b] for j in range(q)])
+                rt = checksums([rtau[k] for k in range(kmax)])
+                del R, rtau, ref
+                cols, taus = {}, {}
+                for c_, t_ in allcs:
+                    cols.update(c_)
+                    taus.update(t_)
+                bad = [j for j in range(q) if cols.get(j) != rc[j]] + [-1 - k for k in range(kmax) if taus.get(k) != rt[k]]
+                out[f"run{rep}"] = {"cols_covered": len(cols) == q, "mismatched": bad[:16], "exact": not bad}
+            dist.barrier()
+            torch.cuda.empty_cache()
+            continue
         mine = {j: A[j * b:(j + 1) * b].cpu().numpy() for j in own}
         mine_tau = {k: tau[k].cpu().numpy() for k in range(kmax) if plan.owns(k)}
         allcols = [None] * world

@@ -38,3 +38,45 @@ def test_invalid_args_without_gpu(tqr):
     h = ctypes.c_void_p()
     assert L.tqr_plan_create(ctypes.byref(h), 100, 64, 32, 1) == -1  # b does not divide m
     assert L.tqr_plan_create(ctypes.byref(h), 96, 96, 24, 1) == -1   # unsupported tile size
+
+
+def test_leading_dimension_bound_without_gpu(tqr):
+    """32 * ldm * sizeof(element) must stay below 2^31 (the engine's 32-bit buffer offsets,
+    include/tqr.h): rejected before any device work."""
+    import ctypes
+    L = tqr.lib()
+    h = ctypes.c_void_p()
+    m = 8388608 + 256  # > 8,388,607 rows: too tall for fp64
+    assert L.tqr_plan_create(ctypes.byref(h), m, 256, 256, 1) == -1
+    # the same shape in fp32 passes the bound and only then needs a device (-4 here, no GPU)
+    st = L.tqr_plan_create(ctypes.byref(h), m, 256, 256, 0)
+    assert st in (-4, 0)
+    if st == 0:
+        L.tqr_plan_destroy(h)
+
+
+def test_invalid_engine_and_batch_args_without_gpu(tqr):
+    import ctypes
+    L = tqr.lib()
+    h = ctypes.c_void_p()
+    assert L.tqr_plan_create_engine(ctypes.byref(h), 256, 256, 64, 1, 7) == -1
+    assert L.tqr_geqrt_host_engine(1, None, None, 256, 256, 256, 64, 0) == -1
+    # only the update types (SAPP = 1, DAPP = 3) batch; GEQRT (0) is rejected
+    ms = ctypes.c_float()
+    assert L.tqr_tile_batch(1, 0, 32, 4, None, 32, None, None, 64, None, 0, ctypes.byref(ms)) == -1
+    assert L.tqr_dist_import(None, None, 0) == -1
+    assert L.tqr_plan_execute(None, None, 0, None, None) == -1
+
+
+def test_flow_plan_export(tqr):
+    """The persistent engine's task list (host only): every panel member and chain segment once."""
+    import ctypes
+    L = tqr.lib()
+    M, N = 12, 8
+    n = L.tqr_flow_plan_export(M, N, 256, 4, None, 0)
+    buf = (ctypes.c_int * (4 * n))()
+    assert L.tqr_flow_plan_export(M, N, 256, 4, buf, n) == n
+    items = [tuple(buf[4 * x:4 * x + 4]) for x in range(n)]
+    panels = [it for it in items if (it[0] & 0xff) != 4]
+    assert len(panels) == sum(M - k for k in range(min(M, N)))
+    assert len(set(items)) == n

@@ -78,16 +78,19 @@ def test_partition_gloo_world2():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("m,n,b,dt,ranks", [(1024, 1024, 128, "f64", 2), (2048, 768, 256, "f64", 2),
-                                            (512, 1024, 64, "f64", 2), (1024, 512, 128, "f32", 2),
-                                            (2048, 2048, 256, "f64", 4)])
-def test_ranks_on_one_gpu_match_single_gpu(m, n, b, dt, ranks):
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("m,n,b,dt,ranks,mode", [(1024, 1024, 128, "f64", 2, "gather"), (2048, 768, 256, "f64", 2, "gather"),
+                                                 (512, 1024, 64, "f64", 2, "gather"), (1024, 512, 128, "f32", 2, "gather"),
+                                                 (2048, 2048, 256, "f64", 4, "gather"),
+                                                 # BASELINE configs[3] shape at full size
+                                                 (65536, 16384, 256, "f64", 2, "checksum")])
+def test_ranks_on_one_gpu_match_single_gpu(m, n, b, dt, ranks, mode):
     env = dict(os.environ, TQR_FLOW_GRID=str(192 // ranks))
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr=127.0.0.1", f"--master-port={port}",
-           os.path.join(HERE, "dist_worker.py"), str(m), str(n), str(b), dt, "0"]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+           os.path.join(HERE, "dist_worker.py"), str(m), str(n), str(b), dt, "0", mode]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=500)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)

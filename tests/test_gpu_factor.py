@@ -118,11 +118,12 @@ def _device_factor(tqr, m, n, b, dtype, seed=5):
     return A0, A, tau
 
 
-@pytest.mark.parametrize("m,n,b", [(16384, 16384, 256), (65536, 4096, 256)])
+@pytest.mark.parametrize("m,n,b", [(16384, 16384, 256), (65536, 4096, 256), (65536, 16384, 256)])
 def test_full_size_properties(tqr, m, n, b):
-    """BASELINE configs[2] (and a tall shape): Q orthogonal => every column norm of R equals
-    that of A, and the diagonal of R is nonzero; R matches an independent QR up to row signs
-    on the leading block."""
+    """BASELINE configs[2] and configs[3] (65536 x 16384, here on one GPU), and a tall shape:
+    Q orthogonal => every column norm of R equals that of A; every tau lies in [1, 2] (tau =
+    2/(1+|v_B|^2) >= 1 for TSQRT reflectors, 2/(v'v) with v0 = 1 for GEQRT); R matches an
+    independent QR (torch) up to row signs on the leading 2048 columns."""
     import torch
     A0, F, tau = _device_factor(tqr, m, n, b, torch.float64)
     R = torch.triu(F.T).T  # (n, m) storage: zero below the diagonal
@@ -139,14 +140,50 @@ def test_full_size_properties(tqr, m, n, b):
     assert err <= 1e-11
 
 
-def test_fp32_device_large(tqr):
+@pytest.mark.parametrize("m", [4096, 32768])
+def test_fp32_device_large(tqr, m):
+    """fp32 storage up to BASELINE configs[4] (32768 x 32768, b = 256) at full size: column norms
+    of R equal those of A (fp32 tolerance 5e-5) and |R| matches torch's fp64 QR of
+    the same (fp32) columns on the leading 1024 columns within the reference's EPSILON-scale
+    relative bound."""
     import torch
-    m = n = 4096
+    n = m
     A0, F, tau = _device_factor(tqr, m, n, 256, torch.float32)
-    R = torch.triu(F.T).T.double()
+    R = torch.triu(F.T).T
     na = torch.linalg.vector_norm(A0.double(), dim=1)
-    nr = torch.linalg.vector_norm(R, dim=1)
+    nr = torch.linalg.vector_norm(R.double(), dim=1)
     assert ((na - nr).abs() / na).max().item() <= 5e-5
+    assert torch.all(tau[tau != 0] >= 1.0 - 1e-6) and torch.all(tau <= 2.0 + 1e-6)
+    c = 1024
+    Rt = torch.linalg.qr(A0[:c, :].double().T.contiguous(), mode="r")[1]
+    Rg = R[:c, :c].T.double()
+    assert ((Rt.abs() - Rg.abs()).abs().max() / Rt.abs().max()).item() <= 1e-4
+    del R, F, A0
+
+
+@pytest.mark.timeout(900)
+def test_config_c3_elementwise_vs_oracle(tqr, oracle):
+    """BASELINE configs[2] (16384 x 16384 fp64, b = 256) elementwise against the oracle (the
+    reference host path restated, run with every host thread this process may use): R, V and tau
+    at the SURVEY.md §8d tolerance max|dF| <= 1e-11 max|F|, tau <= 1e-11 * 2. The oracle's wall
+    time is printed (pytest -s / the log's captured stdout)."""
+    import time
+    m = n = 16384
+    b = 256
+    thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    A = oracle.randzo(m, n, np.float64, seed=5)
+    F = A.copy()
+    T = tqr.geqrt_host(F, b)
+    t0 = time.perf_counter()
+    F_ref, T_ref = oracle.factor(A, b, threads=thr)
+    print(f"c3 oracle: {time.perf_counter() - t0:.1f} s on {thr} threads")
+    del A
+    s = max(1.0, float(np.abs(F_ref).max()))
+    dF = max(float(np.abs(F[j:j + 1024] - F_ref[j:j + 1024]).max()) for j in range(0, n, 1024))
+    dT = max(float(np.abs(T[j * b] - T_ref[j * b]).max()) for j in range(n // b))
+    print(f"c3 elementwise: max|dF| = {dF:.3e} (scale {s:.3e}), max|dtau| = {dT:.3e}")
+    assert dF <= 1e-11 * s
+    assert dT <= 1e-11 * 2
 
 
 def test_legacy_entry_points(tqr, oracle):

@@ -1,0 +1,277 @@
+"""Host-side model of the persistent engine (k_flow): simulates the in-order dequeue of a flow task
+list on W workgroups with the kernel's waits (flow.hpp: panel members pipelined per reflector group
+through Rr/Rc/Rt, chain elements waiting per group for the panel images of the NEXT group, Tc for the
+tile's previous step, Ac for the previous segment's head rows) and per-group durations taken from
+the activity stamps (tools/flowstamps.py). Usage: python tools/sched_sim.py [M] [order]"""
+import ctypes, heapq, os, sys
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpu-tiled-qr-decomposition_amd"))
+
+P = dict(f=29.0, bt=9.3, io_in=4.0, io_wb=2.0, io_img=4.0, t=15.5, c=16.0, e_ld=7.0, e_st=7.0, disp=1.5, W=256, NG=8)
+
+
+def export_list(M, N, b=256, seglen=8):
+    import tqr
+    L = tqr.lib()
+    n = L.tqr_flow_plan_export(M, N, b, seglen, None, 0)
+    buf = (ctypes.c_int * (4 * n))()
+    L.tqr_flow_plan_export(M, N, b, seglen, buf, n)
+    return np.frombuffer(buf, dtype=np.int32).reshape(n, 4).copy()
+
+
+def simulate(items, M, N, ns=2, prm=P, waits=None):
+    NG, W = prm["NG"], prm["W"]
+    wt = waits if waits is not None else {}
+    acc = lambda c, v: wt.__setitem__(c, wt.get(c, 0.0) + max(0.0, v))
+    Rr, Rc, E = {}, {}, {}       # panel (i,k) -> per-group times
+    Tc = {}                      # (i, j, s, k) -> element end (tile (i,j) strip s done at step k)
+    G = {}                       # (k, j, s, e) -> last element's group times (head rows for next segment)
+    workers = [0.0] * W
+    heapq.heapify(workers)
+    busy = 0.0
+    starts = np.zeros(len(items))
+    ends = np.zeros(len(items))
+    for x, (ts, l, m, kk) in enumerate(items):
+        t0 = heapq.heappop(workers) + prm["disp"]
+        typ = ts & 0xff
+        if typ != 4:  # panel member (l, k); l == k: GEQRT
+            i, k = l, kk
+            t = t0
+            if k > 0:
+                t = max([t] + [Tc[(i, k, s, k - 1)] for s in range(ns)])
+            acc("panel Tc wait", t - t0)
+            rr, rc, ee = [0.0] * NG, [0.0] * NG, [0.0] * NG
+            prev = (i - 1, k) if i > k else None
+            for g in range(NG):
+                gs = t if g == 0 else ee[g - 1]
+                if prev:
+                    acc("panel Rr wait", Rr[prev][g] + prm.get("hop", 0.0) - gs)
+                    gs = max(gs, Rr[prev][g] + prm.get("hop", 0.0))
+                rr[g] = gs + prm["io_in"] + prm["f"] + prm["io_wb"]
+                rc[g] = rr[g] + prm["bt"] + prm["io_img"]
+                if prev:
+                    acc("panel Rt wait", E[prev][g] - rc[g])
+                ee[g] = (max(rc[g], E[prev][g]) if prev else rc[g]) + prm["t"]
+            Rr[(i, k)], Rc[(i, k)], E[(i, k)] = rr, rc, ee
+            end = ee[-1]
+        else:
+            s = (ts >> 8) & 0xff
+            i0, i1 = l & 0xffff, l >> 16
+            k, e = kk & 0xffff, kk >> 16
+            j = m
+            rows = ([k] if e == 0 else []) + list(range(i0, i1))
+            t = t0
+            if e > 0:
+                pg = G[(k, j, s, e - 1)]
+            last = None
+            la = "la" if j == k + 1 else "other"
+            for idx, i in enumerate(rows):
+                if k > 0:
+                    acc("chain Tc wait", Tc[(i, j, s, k - 1)] - t)
+                    t = max(t, Tc[(i, j, s, k - 1)])
+                t += prm["e_ld"]
+                rc = Rc[(i, k)]
+                nxt = Rc[(rows[idx + 1], k)][0] if idx + 1 < len(rows) else 0.0
+                g_t = [0.0] * NG
+                for g in range(NG):
+                    need = rc[g + 1] if g + 1 < NG else nxt
+                    st = max(t, rc[g], need)
+                    acc(f"chain Rc wait {la} {'start' if g == 0 and idx == 0 else 'in-elem'}", st - t)
+                    if e > 0 and idx == 0:
+                        acc("chain Ac wait", pg[min(g + 1, NG - 1)] - st)
+                        st = max(st, pg[min(g + 1, NG - 1)])
+                    t = st + prm["c"]
+                    g_t[g] = t
+                t += prm["e_st"]
+                Tc[(i, j, s, k)] = t
+                last = g_t
+            G[(k, j, s, e)] = last
+            end = t
+        starts[x], ends[x] = t0, end
+        busy += end - t0
+        heapq.heappush(workers, end)
+    return ends.max(), starts, ends
+
+
+if __name__ == "__main__":
+    M = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    items = export_list(M, M)
+    w = {}
+    span, s, e = simulate(items, M, M, waits=w)
+    print(f"current order: {len(items)} tasks, simulated makespan {span / 1e3:.1f} ms")
+    for c in sorted(w):
+        print(f"  {c:28s} {w[c] / P['W'] / 1e3:7.2f} ms/WG")
+    p0 = dict(P, f=0.0, bt=0.0, t=0.0)
+    span0, _, _ = simulate(items, M, M, prm=p0)
+    print(f"  with free panel compute (PANEL0): {span0 / 1e3:.1f} ms")
+
+
+def tasks_of(M, N, ns=2, seglen=8, seglen_la=None):
+    """All tasks: ('P', i, k) and ('C', k, j, s, e, i0, i1) with the engine's segmenting."""
+    seglen_la = seglen_la or seglen
+    T = []
+    K = min(M, N)
+    for k in range(K):
+        for i in range(k, M):
+            T.append(("P", i, k))
+        for j in range(k + 1, N):
+            sl = seglen_la if j == k + 1 else seglen
+            nseg = max(1, (M - k - 1 + sl - 1) // sl)
+            for e in range(nseg):
+                i0, i1 = k + 1 + e * sl, min(M, k + 1 + (e + 1) * sl)
+                if M - k - 1 == 0:
+                    i0 = i1 = M
+                for s in range(ns):
+                    T.append(("C", k, j, s, e, i0, i1))
+    return T
+
+
+def to_items(order):
+    out = []
+    for t in order:
+        if t[0] == "P":
+            out.append((0 if t[1] == t[2] else 2, t[1], t[2], t[2]))
+        else:
+            _, k, j, s, e, i0, i1 = t
+            out.append((4 | (s << 8), i0 | (i1 << 16), j, k | (e << 16)))
+    return np.array(out, dtype=np.int64)
+
+
+def greedy_order(M, N, ns=2, seglen=8, seglen_la=None, prm=P, prio="panel"):
+    """List scheduling against the model: each next list slot goes to the earliest-free
+    workgroup; among tasks whose wait targets are all earlier in the list, a task whose first
+    useful work could start by then is preferred by (class, step, column) — panels, then the
+    lookahead column's chains, then other chains — else the one that can start soonest."""
+    seglen_la = seglen_la or seglen
+    NG, W = prm["NG"], prm["W"]
+    T = tasks_of(M, N, ns, seglen, seglen_la)
+    segl = lambda k, j: seglen_la if j == k + 1 else seglen
+    segof = lambda k, j, i: (i - k - 1) // segl(k, j)
+    # dependency (wait-target) lists
+    deps = {}
+    for t in T:
+        if t[0] == "P":
+            _, i, k = t
+            d = []
+            if i > k:
+                d.append(("P", i - 1, k))
+            if k > 0:
+                d += [("Cx", k - 1, k, s, segof(k - 1, k, i)) for s in range(ns)]
+            deps[t] = d
+        else:
+            _, k, j, s, e, i0, i1 = t
+            d = [("P", k, k)] if e == 0 else [("Cx", k, j, s, e - 1)]
+            rows = ([k] if e == 0 else []) + list(range(i0, i1))
+            for i in rows:
+                if i > k:
+                    d.append(("P", i, k))
+                if k > 0:
+                    d.append(("Cx", k - 1, j, s, segof(k - 1, j, i)))
+            deps[t] = d
+    key = lambda t: ("Cx",) + t[1:5] if t[0] == "C" else t
+    succ = {}
+    ndep = {}
+    for t in T:
+        ds = set(deps[t])
+        ndep[key(t)] = len(ds)
+        for d in ds:
+            succ.setdefault(d, []).append(t)
+    Rr, Rc, E, Tc, G = {}, {}, {}, {}, {}
+    workers = [0.0] * W
+    heapq.heapify(workers)
+    notready, ready = [], []
+    cnt = 0
+
+    def ready_time(t):
+        if t[0] == "P":
+            _, i, k = t
+            r = 0.0
+            if k > 0:
+                r = max(Tc[(i, k, s, k - 1)] for s in range(ns))
+            if i > k:
+                r = max(r, Rr[(i - 1, k)][0] - prm["io_in"] - prm["f"] - prm["io_wb"])
+            return r
+        _, k, j, s, e, i0, i1 = t
+        i = k if e == 0 else i0
+        r = max(Rc[(i, k)][0], Rc[(i, k)][1])
+        if k > 0:
+            r = max(r, Tc[(i, j, s, k - 1)])
+        if e > 0:
+            r = max(r, G[(k, j, s, e - 1)][1])
+        return r
+
+    def prio_key(t):
+        if t[0] == "P":
+            return (0, t[2], t[1])
+        _, k, j, s, e, i0, i1 = t
+        return (1 if j == k + 1 else 2, k, j, e, s)
+
+    def push(t):
+        nonlocal cnt
+        cnt += 1
+        heapq.heappush(notready, (ready_time(t), cnt, t))
+
+    for t in T:
+        if ndep[key(t)] == 0:
+            push(t)
+    order = []
+    while notready or ready:
+        tw = workers[0] + prm["disp"]
+        while notready and notready[0][0] <= tw:
+            r, c, t = heapq.heappop(notready)
+            heapq.heappush(ready, (prio_key(t), c, t))
+        if ready:
+            _, _, t = heapq.heappop(ready)
+        else:
+            _, _, t = heapq.heappop(notready)
+        order.append(t)
+        # place t: compute its times with the same rules as simulate()
+        t0 = heapq.heappop(workers) + prm["disp"]
+        if t[0] == "P":
+            _, i, k = t
+            tt = t0
+            if k > 0:
+                tt = max([tt] + [Tc[(i, k, s, k - 1)] for s in range(ns)])
+            rr, rc, ee = [0.0] * NG, [0.0] * NG, [0.0] * NG
+            prev = (i - 1, k) if i > k else None
+            for g in range(NG):
+                gs = tt if g == 0 else ee[g - 1]
+                if prev:
+                    gs = max(gs, Rr[prev][g] + prm.get("hop", 0.0))
+                rr[g] = gs + prm["io_in"] + prm["f"] + prm["io_wb"]
+                rc[g] = rr[g] + prm["bt"] + prm["io_img"]
+                ee[g] = (max(rc[g], E[prev][g]) if prev else rc[g]) + prm["t"]
+            Rr[(i, k)], Rc[(i, k)], E[(i, k)] = rr, rc, ee
+            end = ee[-1]
+        else:
+            _, k, j, s, e, i0, i1 = t
+            rows = ([k] if e == 0 else []) + list(range(i0, i1))
+            tt = t0
+            pg = G[(k, j, s, e - 1)] if e > 0 else None
+            last = None
+            for idx, i in enumerate(rows):
+                if k > 0:
+                    tt = max(tt, Tc[(i, j, s, k - 1)])
+                tt += prm["e_ld"]
+                rc = Rc[(i, k)]
+                nxt = Rc[(rows[idx + 1], k)][0] if idx + 1 < len(rows) else 0.0
+                g_t = [0.0] * NG
+                for g in range(NG):
+                    need = rc[g + 1] if g + 1 < NG else nxt
+                    st = max(tt, rc[g], need)
+                    if pg is not None and idx == 0:
+                        st = max(st, pg[min(g + 1, NG - 1)])
+                    tt = st + prm["c"]
+                    g_t[g] = tt
+                tt += prm["e_st"]
+                Tc[(i, j, s, k)] = tt
+                last = g_t
+            G[(k, j, s, e)] = last
+            end = tt
+        heapq.heappush(workers, end)
+        for u in succ.get(key(t), []):
+            ndep[key(u)] -= 1
+            if ndep[key(u)] == 0:
+                push(u)
+    return order

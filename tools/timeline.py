@@ -25,6 +25,8 @@ items = (ctypes.c_int * (4 * n))()
 assert L.tqr_debug_task_timeline(p.h, tl, n, items) == 0
 T = np.frombuffer(tl, dtype=np.uint64).reshape(n, 3).astype(np.int64)
 I = np.frombuffer(items, dtype=np.int32).reshape(n, 4)
+if os.environ.get("TQR_TIMELINE_DUMP"):
+    np.savez_compressed(os.environ["TQR_TIMELINE_DUMP"], T=T, I=I)
 t0 = T[:, 0].min()
 s = (T[:, 0] - t0) / 100.0  # us (100 MHz)
 e = (T[:, 1] - t0) / 100.0

@@ -1,5 +1,8 @@
-// Microbenchmark: fp64 MFMA (v_mfma_f64_16x16x4_f64, v_mfma_f64_4x4x4_f64) and fp64 vector FMA
+// Microbenchmark: fp64 MFMA (v_mfma_f64_16x16x4_f64, v_mfma_f64_4x4x4_4b_f64), fp32-input MFMA
+// (v_mfma_f32_16x16x4_f32, v_mfma_f32_32x32x2_f32, v_mfma_f32_4x4x1_16b_f32) and fp64 vector FMA
 // throughput on gfx950, with the in-kernel clock (s_memtime / s_memrealtime @100 MHz).
+// Flops per wave-instruction: 16x16x4 f64 2*16*16*4 = 2048; 4x4x4_4b f64 4 blocks * 2*4*4*4 = 512;
+// 16x16x4 f32 2048; 32x32x2 f32 2*32*32*2 = 4096; 4x4x1_16b f32 16 blocks * 2*4*4*1 = 512.
 // Establishes the roofline denominators used in bench.py (DESIGN.md "Roofline").
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -44,6 +47,37 @@ __global__ __launch_bounds__(256) void k_mfma4(double* out, unsigned long long* 
   stamp(clk, 0);
   double s = 0;
   for (int i = 0; i < NACC; ++i) s += acc[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+// SHAPE 0: 16x16x4 f32 (4 acc regs), 1: 32x32x2 f32 (16 acc regs), 2: 4x4x1_16b f32 (4 acc regs)
+template <int SHAPE, int NACC>
+__global__ __launch_bounds__(256) void k_mfma32(float* out, unsigned long long* clk, int iters, float seed) {
+  float a = seed * (threadIdx.x + 1), b = seed * 0.5f - threadIdx.x * 1e-7f;
+  stamp(clk, 1);
+  float s = 0;
+  if constexpr (SHAPE == 1) {
+    f16v acc[NACC];
+    for (int i = 0; i < NACC; ++i) acc[i] = f16v{} + seed * i;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < NACC; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i], 0, 0, 0);
+    }
+    for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][15];
+  } else {
+    f4 acc[NACC];
+    for (int i = 0; i < NACC; ++i) acc[i] = f4{seed, -seed, seed * i, -seed};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < NACC; ++i)
+        acc[i] = SHAPE == 0 ? __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i], 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, acc[i], 0, 0, 0);
+    }
+    for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][3];
+  }
+  stamp(clk, 0);
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
@@ -94,7 +128,10 @@ int main() {
     snprintf(nm, sizeof nm, NAME " %d wave/SIMD", bpc); report(nm, ms, FLOPS, hclk, blocks);
     RUN("mfma_f64_16x16x4 x4acc", (k_mfma<4><<<blocks, 256>>>(out, clk, iters, 1e-3)), (double)blocks * 4 * iters * 4 * 2048.0);
     RUN("mfma_f64_16x16x4 x8acc", (k_mfma<8><<<blocks, 256>>>(out, clk, iters / 2, 1e-3)), (double)blocks * 4 * (iters / 2) * 8 * 2048.0);
-    RUN("mfma_f64_4x4x4 x8acc", (k_mfma4<8><<<blocks, 256>>>(out, clk, iters, 1e-3)), (double)blocks * 4 * iters * 8 * 2048.0);
+    RUN("mfma_f64_4x4x4_4b x8acc", (k_mfma4<8><<<blocks, 256>>>(out, clk, iters, 1e-3)), (double)blocks * 4 * iters * 8 * 512.0);
+    RUN("mfma_f32_16x16x4 x8acc", (k_mfma32<0, 8><<<blocks, 256>>>((float*)out, clk, iters / 2, 1e-3f)), (double)blocks * 4 * (iters / 2) * 8 * 2048.0);
+    RUN("mfma_f32_32x32x2 x4acc", (k_mfma32<1, 4><<<blocks, 256>>>((float*)out, clk, iters / 2, 1e-3f)), (double)blocks * 4 * (iters / 2) * 4 * 4096.0);
+    RUN("mfma_f32_4x4x1_16b x8acc", (k_mfma32<2, 8><<<blocks, 256>>>((float*)out, clk, iters, 1e-3f)), (double)blocks * 4 * iters * 8 * 512.0);
     RUN("v_fma_f64 x8", (k_fma<<<blocks, 256>>>(out, clk, iters * 4, 1.0)), (double)blocks * 256 * iters * 4 * 8 * 2.0);
   }
   return 0;
