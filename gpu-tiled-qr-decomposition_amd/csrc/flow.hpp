@@ -258,6 +258,22 @@ __device__ __forceinline__ bool sync_point(bool ok0, int* sflag, int& par) {
   asm volatile("" ::: "memory");
   return *(volatile int*)slot != 0;
 }
+// A group's sync point inside a segment: only the LDS-DMA of this group (issued in the previous
+// group's phase 1) and everything older must have landed; the N youngest operations — the
+// previous group's head-row stores and this group's head-row loads, issued after that DMA — may
+// still be in flight (the stores are read back by this workgroup only, the loads are waited for
+// at their first use).
+template <int N>
+__device__ __forceinline__ bool sync_point_cnt(bool ok0, int* sflag, int& par) {
+  int* slot = sflag + 40 + par;
+  par ^= 1;
+  if (threadIdx.x == 0) *slot = ok0 ? 1 : 0;
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  return *(volatile int*)slot != 0;
+}
 // The first group's sync point of an element: everything older than the element's own strip and
 // head loads (the previous element's stores, this group's LDS-DMA) must be complete, the NX
 // loads issued after them need not be — phase 1 waits for each strip row as it reaches it (the
@@ -542,6 +558,25 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
 }
 
 // ---- chain tasks ---------------------------------------------------------------------------
+// Element hand-over inside the last group's phase 2 (apply_x post hook): once row pair h-1 of the
+// strip is final, it is stored (write-through) and the same registers start loading pair h-1 of
+// the next element's strip — the strip's 512 B per lane out and in ride the MFMA stream instead
+// of sitting between two elements (what-if without strip I/O: -19 ms at 16384^2).
+template <int B, typename S>
+struct XPipe {
+  __amdgpu_buffer_rsrc_t out, in;  // this element's strip / the next element's (same columns)
+  unsigned base;
+  __device__ __forceinline__ void xfer(int h, double (&X)[Geo<B>::NKS]) const {
+    const unsigned so = base + 8 * h * sizeof(S);
+    st_pair<S>(out, so, X[2 * h], X[2 * h + 1]);
+    ld_pair<S>(in, so, X[2 * h], X[2 * h + 1]);
+  }
+  __device__ __forceinline__ void at(int h, double (&X)[Geo<B>::NKS]) const {
+    if (h >= 1) xfer(h - 1, X);  // pair h-1 retired one k-step pair ago
+  }
+  __device__ __forceinline__ void fin(double (&X)[Geo<B>::NKS]) const { xfer(Geo<B>::NKS / 2 - 1, X); }
+};
+
 // Elements: UNMQR(k,j) (segment 0 only, GE-type, the strip of tile (k,j) is X) and TSMQR(i,j,k)
 // for i in [i0,i1) (TS-type: X = strip of tile (i,j), head rows = strip of tile (k,j), group by
 // group, prefetched one group ahead into registers). Per reflector group g, in every wave:
@@ -583,7 +618,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   bool dma_next = false;  // group 0 of the next element already in flight
   PanelView<NG> pv;
   pv.init(sflag + 48);
-  int tc_pf = -1;  // thread 0: Tc of the next element's tile, loaded one group ahead
+  int tc_pf = -1;  // thread 0: Tc of the next element's tile, loaded two groups ahead
+  bool xin = false;  // this element's strip was loaded during the previous element's last phase 2
   // multi-GPU, panel owned by another rank: per-member flags forwarded by the owner
   const bool remote = a.dist && (k % a.world != a.rank);
   int* const rf = a.Rf + (size_t)k * P * NG;
@@ -620,7 +656,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     }
     dma_next = false;
 #ifndef TQR_DIAG_NOSTRIP
-    if (active) load_strip_pair<B, S>(X, Xt, ldm, col);
+    if (active && !xin) load_strip_pair<B, S>(X, Xt, ldm, col);
 #endif
     // head rows: written by another workgroup before this segment or by this one (sc1 loads
     // for both). The UNMQR element (i == k, GE-type V) runs the very same TSMQR code with a zero
@@ -645,6 +681,15 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         FST(g == 0 ? 22 : 21);
 #endif
+        if (t == 0 && g + 1 == NG) {
+          // last group: may the next element's strip stream in during this phase 2? (its tile
+          // must have received step k-1: Tc, loaded two groups ahead)
+#ifdef TQR_DIAG_NOSTRIP
+          sflag[44] = 0;
+#else
+          sflag[44] = (NG > 1 && has_next && (k == 0 || tc_pf >= k)) ? 1 : 0;
+#endif
+        }
         if (t == 0) {
           // first element of a later segment: head rows of group g+1 (prefetched below) final?
           if (i == ifirst && seg > 0 && g + 1 < NG) ok = spin_ge(&acg[g + 1], seg, err);
@@ -656,10 +701,17 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         FST(j == k + 1 ? 20 : 0);  // Rc wait inside an element (lookahead column / other)
         // group 0: the strip / head loads of this element may still be in flight
         constexpr int NX = G::NKS / 2 + (FLOW_PF ? G::NRI : 0);
-        if (!(g == 0 ? sync_point_first<NX>(ok, sflag, par, active) : sync_point<true>(ok, sflag, par)))
+        // full drain where a publish follows: the segment's last element (head rows, Ac) and the
+        // first group after a streamed hand-over (the previous element's strip stores, Tc)
+        const bool full = !has_next || (xin && g == 1);
+        constexpr int NH = FLOW_PF ? 2 * G::NRI : G::NRI;  // head stores + next head loads
+        if (!(g == 0 ? sync_point_first<NX>(ok, sflag, par, active)
+                     : full ? sync_point<true>(ok, sflag, par) : sync_point_cnt<NH>(ok, sflag, par)))
           return false;
       }
-      if (g == 0 && pending) {
+      // the previous element's strip stores are drained: at group 0 (stored before this
+      // element's loads) or, after a streamed hand-over (stores interleaved with the loads), at 1
+      if (g == (xin ? 1 : 0) && pending) {
         publish_after_drain(pending, 1);
         pending = nullptr;
       }
@@ -672,7 +724,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
           fl_pf = g + 1 < NG ? rf + (size_t)i * NG + g + 1 : has_next ? rf + (size_t)inext * NG : nullptr;
           fl_pv = fl_pf ? ld_sys(fl_pf) : 0;
         }
-        if (g + 1 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
+        if (g + 2 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
       }
       FST(7);
       if (!FLOW_PF && active) load_head_buf<B, S, 16>(H, hrs, hoff + g * IB * sizeof(S));  // 2 waves/SIMD
@@ -708,7 +760,19 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       }
 #endif
       FST(14);
-      if (active) apply_x<B, true, FLOW_PF>(Vs, X, W, 0);
+      bool pipe = false;
+      if (g + 1 == NG) pipe = *(volatile int*)(sflag + 44) != 0;  // (written before this sync point)
+      if (active) {
+        if (pipe) {
+          S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
+          const XPipe<B, S> xp{uniform_rsrc(Xt + (size_t)col * ldm), uniform_rsrc(Xn + (size_t)col * ldm),
+                               (unsigned)((((size_t)(t & 15)) * ldm + 2 * ((t & 63) >> 4)) * sizeof(S))};
+          apply_x<B, true, FLOW_PF, NoHook, XPipe<B, S>>(Vs, X, W, 0, NoHook(), xp);
+        } else {
+          apply_x<B, true, FLOW_PF>(Vs, X, W, 0);
+        }
+      }
+      if (g + 1 == NG) xin = pipe;
       FST(13);
       if (FLOW_PF) {
 #pragma unroll
@@ -720,7 +784,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     };
     if (!groups()) return;
 #ifndef TQR_DIAG_NOSTRIP
-    if (active) store_strip_pair<B, S>(X, Xt, ldm, col);
+    if (active && !xin) store_strip_pair<B, S>(X, Xt, ldm, col);
 #endif
     pending = tc(i);
     FST(4);

@@ -216,9 +216,18 @@ __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const do
   }
 }
 
-template <int B, bool HEAD, bool PF = true, typename Hook = NoHook>
+// Post hook of apply_x: at(h, X) runs after the MFMAs of row pair h (X[2h], X[2h+1] final once
+// they retire), fin(X) after the loop — the chain streams its strip out / the next one in there.
+struct NoPost {
+  template <typename XA>
+  __device__ __forceinline__ void at(int, XA&) const {}
+  template <typename XA>
+  __device__ __forceinline__ void fin(XA&) const {}
+};
+template <int B, bool HEAD, bool PF = true, typename Hook = NoHook, typename Post = NoPost>
 __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&X)[Geo<B>::NKS],
-                                        const double (&W)[Geo<B>::NRI], int ks0, const Hook& hook = Hook()) {
+                                        const double (&W)[Geo<B>::NRI], int ks0, const Hook& hook = Hook(),
+                                        const Post& post = Post()) {
   using g = Geo<B>;
   constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP;
   const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
@@ -262,7 +271,9 @@ __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&
 #pragma unroll
         for (int r = 0; r < NRI; ++r) bc[u][r] = bn[u][r];
     }
+    post.at(kb / 2, X);
   }
+  post.fin(X);
   for (int m = NKS / 2; m < Hook::STEPS; ++m) hook.step(m);
 }
 
