@@ -35,6 +35,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "gpu-tiled-qr-decomposition_amd"))
 
 FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X datasheet fp64 matrix peak (DESIGN.md "Roofline")
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X fp32 matrix peak (MI355X_MICROARCH.md; 152-155 measured)
 METRIC = "fp64 QR GFLOP/s and %MFMA-peak, dense m×n, at 1/2/4/8 MI355X"
 
 
@@ -161,7 +162,8 @@ def main():
     ap.add_argument("--cols", type=int, default=None, help="n (default 16384)")
     ap.add_argument("--tile", type=int, default=256)
     ap.add_argument("--storage", choices=["f64", "f32"], default="f64",
-                    help="matrix element type (arithmetic is fp64 either way; f32 = BASELINE configs[4])")
+                    help="matrix element type: f64 (fp64 MFMA chains) or f32 (fp32 MFMA chains, fp64 panel "
+                         "factorisation; BASELINE configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=6144)
     args = ap.parse_args()
@@ -239,15 +241,17 @@ def main():
     uf = update_flops(m, n, b)
     # per GPU: its share of the update flops (1/N of the job at N > 1) over its launch time
     achieved = uf / world / (st["ms_update"] * 1e-3) / 1e12 if st["ms_update"] > 0 else None
+    peak = FP64_MFMA_PEAK_TFLOPS if args.storage == "f64" else FP32_MFMA_PEAK_TFLOPS
     pmc = load_pmc(m, n, b, args.storage) if world == 1 else None
     traffic = pmc.get("update_hbm_bytes_per_launch") if pmc else None
     roof = {
         "bound": "mfma",
-        "kernel": "k_flow (persistent engine; TSMQR/UNMQR strips on v_mfma_f64_4x4x4_4b_f64)",
+        "kernel": "k_flow (persistent engine; TSMQR/UNMQR strips on " +
+                  ("v_mfma_f64_4x4x4_4b_f64)" if args.storage == "f64" else "v_mfma_f32_16x16x4_f32)"),
         "achieved": round(achieved, 3) if achieved else None,
-        "peak": FP64_MFMA_PEAK_TFLOPS,
+        "peak": peak,
         "unit": "TFLOP/s",
-        "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4) if achieved else None,
+        "frac": round(achieved / peak, 4) if achieved else None,
         "traffic": traffic,
         "executed_flops": pmc.get("executed_mfma_flops") if pmc else None,
         "mfma_util": round(pmc["mfma_util"], 4) if pmc and pmc.get("mfma_util") is not None else None,
@@ -256,7 +260,7 @@ def main():
         "avg_launch_ms": round(st["ms_update"] / max(1, st["n_update"]), 4),
         "algorithmic_flops_per_launch": round(uf / max(1, st["n_update"])),
         "panel_kernel_ms_total": round(st["ms_panel"], 3),
-        "whole_factorisation_frac_of_peak": round(value / 1e3 / (world * FP64_MFMA_PEAK_TFLOPS), 4),
+        "whole_factorisation_frac_of_peak": round(value / 1e3 / (world * peak), 4),
     }
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -277,7 +281,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": args.storage,  # the chains' MFMA arithmetic (the panel factorises in fp64 either way)
             "data": "synthetic (RANDZO distribution, device-generated)",
             "config": {"workload": f"tiled QR {m}x{n} {args.storage} storage, tile {b} (BASELINE configs[{cfg}])", "m": m, "n": n,
                        "tile": b, "parallelism": "single GPU" if world == 1 else

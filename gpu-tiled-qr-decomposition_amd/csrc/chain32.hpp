@@ -1,0 +1,347 @@
+// fp32 chain of the persistent engine: fp32 storage, fp32 arithmetic on v_mfma_f32_16x16x4_f32
+// (BASELINE configs[4], 32768^2 fp32). Included by flow.hpp (uses its sync / DMA / counter helpers).
+//
+// The same chain task as flow_chain (UNMQR(k,j) then TSMQR(i,j,k) for the rows of a segment, on a
+// 128-column strip, 8 waves x 16 columns), with the fp32 MFMA at 64 flop/clk/SIMD — twice the fp64
+// 4x4x4 form's rate (profiles/r02/ubench_mfma.txt: 152-155 vs 67-69 TF/s).
+//
+// Register layout (per wave, 16 columns, lane = 16x + y, x = lane >> 4, y = lane & 15): the f32
+// 16x16x4 MFMA takes A[i][k] from lane 16k + i, B[k][j] from lane 16k + j and holds D[4x + r][y]
+// in register r of lane 16x + y (probed: tools/ubench/mfma_probe32.hip, profiles/r02/
+// ubench_mfma_probe32.txt — NOT the f64 16x16x4 form's D[4r + x][y]). A strip tile mt (16 rows)
+// therefore sits with row 16mt + 4x + r in register r of lane x — four consecutive rows per lane,
+// so the strip moves as 16-B accesses — and the same register is the B operand of k-step (mt, r)
+// of Z = V^T X (k = x <-> row 16mt + 4x + r). Z, W and the head rows share the layout: reflector
+// (row) 16mi + 4x + r in register r.
+//   * X: the strip of tile (i,j), NMT float4 registers (64 VGPRs at b = 256);
+//   * Hd: the strip of the chain's head tile (k,j) stays in registers for the whole segment (64
+//     VGPRs): no head-row traffic inside a segment; the first element of a later segment loads it
+//     group by group behind the previous segment (Ac), the last one stores it group by group;
+//     Hd is rotated by NMI tiles per group, so the current group's rows are always Hd[0..NMI);
+//   * per group: Z = Hd[0..NMI) + V^T X (NMT x 4 x NMI MFMAs), W = -T^T Z (4 NPR), Hd += W,
+//     X += V W (NMT x 4 x NMI); the UNMQR element runs Z = V^T Hd, Hd += V W (explicit GE V).
+// The images (VA, VB, TP; tiles.hpp Geo32) are written by the panel task from its fp64 LDS block
+// (the panel itself factorises in fp64 and stores fp32 V, R, tau) and LDS-DMA'd like the fp64 ones.
+#pragma once
+
+namespace tqr {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// the MFMA row index i of A / D <-> the tile-local row or reflector: identity for this form
+__device__ __forceinline__ int sig16(int y) { return y; }
+__device__ __forceinline__ f4v mfma16(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void st_f4(__amdgpu_buffer_rsrc_t rs, unsigned off, f4v v, int aux_sc1 = 1) {
+  __attribute__((ext_vector_type(4))) unsigned u = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                                                     __float_as_uint(v[3])};
+  if (aux_sc1) __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 16);
+  else __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 0);
+}
+__device__ __forceinline__ f4v ld_f4(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  const auto u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+  return f4v{__uint_as_float(u[0]), __uint_as_float(u[1]), __uint_as_float(u[2]), __uint_as_float(u[3])};
+}
+
+// Panel side: the fp32 chain's images of one reflector group from the panel's fp64 LDS block (rows
+// in the paired order of flow_panel: tile row R at LDS row vimg_inv(R), columns permuted by pc) and
+// its T (row-major, pitch TP). All panel threads; 16-B write-through stores.
+template <int B>
+__device__ __noinline__ void write_images32(const double* Vs, const double* Ts, __amdgpu_buffer_rsrc_t rv,
+                                            __amdgpu_buffer_rsrc_t rt) {
+  using G = Geo<B>;
+  using G32 = Geo32<B>;
+  constexpr int NMI = G32::NMI, VP = G::VP, TP = G::TP;
+  auto V = [&](int R, int c) { return (float)Vs[vimg_inv(R) * VP + G::pc(c)]; };
+  for (int idx = threadIdx.x; idx < G32::VA / 4; idx += blockDim.x) {  // VA chunks
+    const int lane = idx & 63, mc = idx >> 6, ch = mc % NMI, mt = mc / NMI, x = lane >> 4, y = lane & 15;
+    f4v v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = ch * 4 + e, r = q / NMI, mi = q % NMI;
+      v[e] = V(16 * mt + 4 * x + r, 16 * mi + sig16(y));
+    }
+    st_f4(rv, 16u * idx, v);
+  }
+  for (int idx = threadIdx.x; idx < G32::VB / 4; idx += blockDim.x) {  // VB chunks
+    const int lane = idx & 63, mc = idx >> 6, wi = mc % NMI, mt = mc / NMI, x = lane >> 4, y = lane & 15;
+    f4v v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = V(16 * mt + sig16(y), 16 * wi + 4 * x + r);
+    st_f4(rv, 16u * (G32::VA / 4 + idx), v);
+  }
+  for (int idx = threadIdx.x; idx < G32::TIMG * 2 / 4; idx += blockDim.x) {  // TP chunks (+ zero pad)
+    const int lane = idx & 63, pr = idx >> 6, x = lane >> 4, y = lane & 15;
+    int mi = 0, wi = 0;
+    for (int c = 0, q = 0; q < NMI * NMI; ++q) {  // pair pr -> (mi <= wi), wi-major
+      const int w_ = q / NMI, m_ = q % NMI;
+      if (m_ > w_) continue;
+      if (c++ == pr) { mi = m_; wi = w_; }
+    }
+    f4v v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = pr < G32::NPR ? (float)(-Ts[(16 * mi + 4 * x + r) * TP + 16 * wi + sig16(y)]) : 0.0f;
+    st_f4(rt, 16u * idx, v);
+  }
+}
+
+// LDS operand reads: NMI float4 chunks of tile mt for this lane
+template <int N>
+__device__ __forceinline__ void ld_chunks(float (&a)[4 * N], const float* img, int mt, int lane) {
+  const f4v* p = reinterpret_cast<const f4v*>(img) + (mt * N) * 64 + lane;
+#pragma unroll
+  for (int c = 0; c < N; ++c) {
+    const f4v v = p[c * 64];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a[4 * c + e] = v[e];
+  }
+}
+
+// One reflector group applied to a strip (X) with head accumulator Hg (TS) or none (GE, UNMQR:
+// the strip is the head tile itself). Phase 1 carries the hook (next group's LDS-DMA).
+template <int B, bool TS, typename Hook>
+__device__ __forceinline__ void apply32(const float* VA, const float* VB, const float* TPi, f4v (&X)[Geo32<B>::NMT],
+                                        f4v (&Hg)[Geo32<B>::NMT], const Hook& hook) {
+  using G32 = Geo32<B>;
+  constexpr int NMT = G32::NMT, NMI = G32::NMI;
+  const int lane = threadIdx.x & 63;
+  f4v Z[NMI];
+#pragma unroll
+  for (int mi = 0; mi < NMI; ++mi) Z[mi] = TS ? Hg[mi] : f4v{0.f, 0.f, 0.f, 0.f};
+  // phase 1: Z += V^T X, operands of tile mt+1 read under the MFMAs of tile mt
+  float ac[4 * NMI], an[4 * NMI];
+  ld_chunks<NMI>(ac, VA, 0, lane);
+#pragma unroll
+  for (int mt = 0; mt < NMT; ++mt) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    hook.step(mt);
+    if (mt + 1 < NMT) ld_chunks<NMI>(an, VA, mt + 1, lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int mi = 0; mi < NMI; ++mi) Z[mi] = mfma16(ac[r * NMI + mi], X[mt][r], Z[mi]);
+#pragma unroll
+    for (int e = 0; e < 4 * NMI; ++e) ac[e] = an[e];
+  }
+  for (int m = NMT; m < Hook::STEPS; ++m) hook.step(m);
+  hook.mid();
+  // W = -T^T Z (upper-triangular T: tile pairs mi <= wi, wi-major in the image)
+  f4v W[NMI];
+  {
+    float tp[4 * G32::NPR];
+    ld_chunks<G32::NPR>(tp, TPi, 0, lane);
+#pragma unroll
+    for (int wi = 0, pr = 0; wi < NMI; ++wi) {
+      W[wi] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int mi = 0; mi <= wi; ++mi, ++pr)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) W[wi] = mfma16(tp[4 * pr + r], Z[mi][r], W[wi]);
+    }
+  }
+  if (TS) {
+#pragma unroll
+    for (int wi = 0; wi < NMI; ++wi) Hg[wi] += W[wi];
+  }
+  // phase 2: X += V W, two tiles interleaved (dependent-accumulator latency 40 > issue 32 cycles)
+  float b0[4 * NMI], b1[4 * NMI];
+#pragma unroll
+  for (int mt = 0; mt < NMT; mt += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    ld_chunks<NMI>(b0, VB, mt, lane);
+    if (mt + 1 < NMT) ld_chunks<NMI>(b1, VB, mt + 1, lane);
+#pragma unroll
+    for (int wi = 0; wi < NMI; ++wi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        X[mt] = mfma16(b0[4 * wi + r], W[wi][r], X[mt]);
+        if (mt + 1 < NMT) X[mt + 1] = mfma16(b1[4 * wi + r], W[wi][r], X[mt + 1]);
+      }
+  }
+}
+
+// Strip / head tile I/O: tile mt of the strip at column col0 + y, rows 16mt + 4x .. + 3.
+template <int B>
+struct Strip32 {
+  __amdgpu_buffer_rsrc_t rs;
+  unsigned base;
+  __device__ __forceinline__ Strip32(float* tile, size_t ldm, int col0) {
+    const int lane = threadIdx.x & 63;
+    rs = uniform_rsrc(tile + (size_t)col0 * ldm);
+    base = (unsigned)(((size_t)(lane & 15) * ldm + 4 * (lane >> 4)) * sizeof(float));
+  }
+  __device__ __forceinline__ unsigned off(int mt) const { return base + 64u * mt; }
+};
+
+template <int B>
+__device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, int i1_, int j_, int k_, int seg_,
+                                          double* lds, int* sflag) {
+  const int s = uni(s_), i0 = uni(i0_), i1 = uni(i1_), j = uni(j_), k = uni(k_), seg = uni(seg_);
+  using G = Geo<B>;
+  using G32 = Geo32<B>;
+  constexpr int NG = G::NG, NMT = G32::NMT, NMI = G32::NMI, BUF = Img<B, float>::V + Img<B, float>::T;
+  float* A = (float*)a.A;
+  const size_t ldm = a.ldm;
+  const int t = threadIdx.x, w = t >> 6;
+  const int col = s * FLOW_SW + 16 * w;
+  const bool active = B % FLOW_SW == 0 || col < B;
+  float* At = A + (size_t)j * B * ldm + (size_t)k * B;
+  double* const wk = uni(a.Wk[k]);
+  const int P = uni(a.p), Q = uni(a.q), NS = uni(a.ns);
+  int* const err = uni(a.err);
+  int* const Tc = uni(a.Tc);
+  auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B, float>(P, i_, k, g_); };
+  auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B, float>(P, i_, k, g_); };
+  int* const rc = &a.Rc[(size_t)k * NG];
+  int* const acg = &a.Ac[(((size_t)k * Q + j) * NS + s) * NG];
+  auto tc = [&](int i) { return &Tc[((size_t)i * Q + j) * NS + s]; };
+  f4v X[NMT], Hd[NMT];
+  int buf = 0, par = 0;
+  int* pending = nullptr;
+  bool dma_next = false;
+  PanelView<NG> pv;
+  pv.init(sflag + 48);
+  int tc_pf = -1;
+  const bool remote = a.dist && (k % a.world != a.rank);
+  int* const rf = a.Rf + (size_t)k * P * NG;
+  int* fl_pf = nullptr;
+  int fl_pv = 0;
+  auto ready = [&](int i_, int g_) -> bool {
+    if (!remote) return pv.ensure(rc, g_, i_ - k + 1, err, false);
+    int* fp = rf + (size_t)i_ * NG + g_;
+    if (fp == fl_pf && fl_pv >= 1) return true;
+    return spin_ge(fp, 1, err, true);
+  };
+  const Strip32<B> hs(At, ldm, col);  // the head tile's strip
+  FST(6);
+  const int ifirst = seg == 0 ? k : i0;
+  for (int i = ifirst; i < i1 || i == k; i = (i == k ? i0 : i + 1)) {
+    const bool ts = i != k;
+    const bool head_in = ts && i == ifirst;  // first element of a later segment: head arrives per group
+    {
+      bool ok = true;
+      if (t == 0) {
+        if (head_in) ok = spin_ge(&acg[0], seg, err);
+        FST(9);
+        if (ok && k > 0 && tc_pf < k) ok = spin_ge(tc(i), k, err);
+        tc_pf = -1;
+        FST(8);
+        if (ok && !dma_next) ok = ready(i, 0);
+      }
+      FST(j == k + 1 ? 18 : 19);
+      if (!sync_point<false>(ok, sflag, par)) return;
+    }
+    FST(7);
+    float* Xt = ts ? A + (size_t)j * B * ldm + (size_t)i * B : At;
+    if (!dma_next) {
+      DmaJob<B, float> d{lds + buf * BUF, vimg(i, 0), timg(i, 0), sflag};
+      for (int m = 0; m < DmaJob<B, float>::STEPS; ++m) d.step(m);
+    }
+    dma_next = false;
+    const Strip32<B> xs(Xt, ldm, col);
+    if (active) {
+      if (ts) {
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) X[mt] = ld_f4(xs.rs, xs.off(mt));
+        if (head_in)
+#pragma unroll
+          for (int mi = 0; mi < NMI; ++mi) Hd[mi] = ld_f4(hs.rs, hs.off(mi));
+      } else {  // UNMQR: the head tile's strip is the operand, and stays as the segment's head
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) Hd[mt] = ld_f4(hs.rs, hs.off(mt));
+      }
+    }
+    FST(4);
+    const int inext = (i == k) ? i0 : i + 1;
+    const bool has_next = inext < i1;
+    auto groups = [&]() -> bool {
+      for (int g = 0; g < NG; ++g) {
+        {
+          bool ok = true;
+          if (t == 0) {
+            if (head_in && g + 1 < NG) ok = spin_ge(&acg[g + 1], seg, err);  // head rows of g+1 final
+            if (ok) {
+              if (g + 1 < NG) ok = ready(i, g + 1);
+              else if (has_next) ok = ready(inext, 0);
+            }
+          }
+          FST(j == k + 1 ? 20 : 0);
+          if (!sync_point<true>(ok, sflag, par)) return false;
+        }
+        if (g == 0 && pending) {
+          publish_after_drain(pending, 1);
+          pending = nullptr;
+        }
+        if (!has_next && g > 0) publish_after_drain(&acg[g - 1], 1);
+        if (t == 0) {
+          if (!remote) {
+            pv.prefetch(rc, false);
+          } else {
+            fl_pf = g + 1 < NG ? rf + (size_t)i * NG + g + 1 : has_next ? rf + (size_t)inext * NG : nullptr;
+            fl_pv = fl_pf ? ld_sys(fl_pf) : 0;
+          }
+          if (g + 1 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
+        }
+        FST(7);
+        const float* img = reinterpret_cast<const float*>(lds + buf * BUF);
+        const float* VA = img;
+        const float* VB = img + G32::VA;
+        const float* TPi = img + 2 * Img<B, float>::V;
+        const int gd = g + 1 < NG ? g + 1 : has_next ? 0 : g, id = g + 1 < NG ? i : has_next ? inext : i;
+        DmaJob<B, float> d{lds + (buf ^ 1) * BUF, vimg(id, gd), timg(id, gd), sflag};
+        dma_next = g + 1 == NG && has_next;
+        if (active) {
+          if (ts) {
+            // next group's head rows (first element of a later segment) ride this group
+            if (head_in && g + 1 < NG)
+#pragma unroll
+              for (int mi = 0; mi < NMI; ++mi) Hd[NMI + mi] = ld_f4(hs.rs, hs.off((g + 1) * NMI + mi));
+            apply32<B, true>(VA, VB, TPi, X, Hd, d);
+            FST(13);
+            if (!has_next)  // segment's last element: the group's head rows leave (write-through)
+#pragma unroll
+              for (int mi = 0; mi < NMI; ++mi) st_f4(hs.rs, hs.off(g * NMI + mi), Hd[mi]);
+            // rotate the head: the next group's rows to Hd[0..NMI)
+            f4v tmp[NMI];
+#pragma unroll
+            for (int mi = 0; mi < NMI; ++mi) tmp[mi] = Hd[mi];
+#pragma unroll
+            for (int mt = 0; mt + NMI < NMT; ++mt) Hd[mt] = Hd[mt + NMI];
+#pragma unroll
+            for (int mi = 0; mi < NMI; ++mi) Hd[NMT - NMI + mi] = tmp[mi];
+            FST(2);
+          } else {
+            apply32<B, false>(VA, VB, TPi, Hd, Hd, d);
+            FST(13);
+          }
+        } else {
+          for (int m = 0; m < DmaJob<B, float>::STEPS; ++m) d.step(m);
+        }
+        buf ^= 1;
+      }
+      return true;
+    };
+    if (!groups()) return;
+    if (active) {
+      if (ts) {
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) st_f4(xs.rs, xs.off(mt), X[mt]);
+      } else if (!has_next) {  // a lone UNMQR (last step): its head tile strip is the result
+#pragma unroll
+        for (int mt = 0; mt < NMT; ++mt) st_f4(hs.rs, hs.off(mt), Hd[mt]);
+      }
+    }
+    pending = tc(i);
+    FST(4);
+  }
+  sync_point<true>(true, sflag, par);
+  if (pending) publish_after_drain(pending, 1);
+  publish_after_drain(&acg[NG - 1], 1);
+  FST(4);
+}
+
+}  // namespace tqr

@@ -67,6 +67,9 @@ __device__ unsigned long long g_ttl[3 << 18];     // task timeline (first 2^18 t
 namespace tqr {
 static_assert(FST_N <= 24, "g_fst holds 24 categories per workgroup");
 static_assert(Geo<256>::TPIMG == 1024 && Geo<16>::TPIMG == 256, "host tpimg_doubles mirrors Geo::TPIMG");
+static_assert(Img<256, float>::V == 8192 && Img<256, float>::T == 384 && Img<16, float>::V == 256 && Img<16, float>::T == 128 &&
+                  Img<64, float>::V == 2048 && Img<64, float>::T == 384,
+              "host wk_bytes mirrors Img<B, float>");
 static_assert(Geo<256>::TPK <= Geo<256>::TSZ && Geo<16>::TPK <= Geo<16>::TSZ, "packed T fits the Gram buffer");
 
 template <int B>
@@ -305,15 +308,12 @@ static void get_kernels(kfn* p, kfn* u, kfn* t) {
 typedef void (*ffn)(FlowArgs);
 template <int B, typename S>
 static ffn get_flow() { return k_flow<B, S>; }
-static size_t lds_flow(int b) {
+static size_t lds_flow(int b, int dtype) {
   int d = 0;
-  switch (b) {
-    case 16: d = flow_lds_doubles<16>(); break;
-    case 32: d = flow_lds_doubles<32>(); break;
-    case 64: d = flow_lds_doubles<64>(); break;
-    case 128: d = flow_lds_doubles<128>(); break;
-    case 256: d = flow_lds_doubles<256>(); break;
-  }
+#define TQR_L(BB) \
+  case BB: d = dtype == TQR_F64 ? flow_lds_doubles<BB, double>() : flow_lds_doubles<BB, float>(); break;
+  switch (b) { TQR_L(16) TQR_L(32) TQR_L(64) TQR_L(128) TQR_L(256) }
+#undef TQR_L
   return (size_t)d * sizeof(double) + 512;  // + task index, sync-point verdicts, Rc view, FST sums
 }
 static ffn resolve_flow(int b, int dtype) {
@@ -322,7 +322,7 @@ static ffn resolve_flow(int b, int dtype) {
   case BB: f = dtype == TQR_F64 ? get_flow<BB, double>() : get_flow<BB, float>(); break;
   switch (b) { TQR_F(16) TQR_F(32) TQR_F(64) TQR_F(128) TQR_F(256) }
 #undef TQR_F
-  if (f && hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_flow(b)) != hipSuccess)
+  if (f && hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_flow(b, dtype)) != hipSuccess)
     return nullptr;
   return f;
 }
@@ -336,6 +336,59 @@ struct FlowPlan {
   std::vector<Item> items;
   bool est_order = false;
 };
+
+// Is a flow task list topological for the engine's in-task waits? Every task must come after
+// every task it waits on (in-order dequeue then guarantees progress, flow.hpp header):
+//   panel (i,k):        panel (i-1,k); the chain segments of step k-1, column k, holding row i;
+//   chain (k,j,s,e):    segment e-1 (head rows) or, for e = 0, GEQRT(k) and the step-(k-1)
+//                       segment holding row k; for each of its rows i: panel (i,k) and the
+//                       step-(k-1) segment holding row i.
+// Segment boundaries are read from the list itself (any segment lengths).
+static bool flow_list_topological(const std::vector<Item>& L, int p, int q, int ns) {
+  std::map<std::pair<int, int>, int> ppos;                       // (i, k) -> position
+  std::map<std::tuple<int, int, int, int>, int> cpos;            // (k, j, s, e) -> position
+  std::map<std::tuple<int, int, int, int>, int> rowpos;          // (k, j, s, row) -> position
+  for (int x = 0; x < (int)L.size(); ++x) {
+    const Item& it = L[x];
+    const int ty = it.ts & 0xff;
+    if (ty == T_CHAIN) {
+      const int s = (it.ts >> 8) & 0xff, k = it.k & 0xffff, e = it.k >> 16, j = it.m, i0 = it.l & 0xffff, i1 = it.l >> 16;
+      if (!cpos.emplace(std::make_tuple(k, j, s, e), x).second) return false;
+      if (e == 0) rowpos[std::make_tuple(k, j, s, k)] = x;
+      for (int i = i0; i < i1; ++i) rowpos[std::make_tuple(k, j, s, i)] = x;
+    } else if (ty == QRS || ty == QRD) {
+      if (!ppos.emplace(std::make_pair(it.l, it.k), x).second) return false;
+    } else {
+      return false;
+    }
+  }
+  auto before = [&](auto& mp, const auto& key, int x) {
+    auto f = mp.find(key);
+    return f != mp.end() && f->second < x;
+  };
+  for (int x = 0; x < (int)L.size(); ++x) {
+    const Item& it = L[x];
+    const int ty = it.ts & 0xff;
+    if (ty == T_CHAIN) {
+      const int s = (it.ts >> 8) & 0xff, k = it.k & 0xffff, e = it.k >> 16, j = it.m, i0 = it.l & 0xffff, i1 = it.l >> 16;
+      if (e > 0 && !before(cpos, std::make_tuple(k, j, s, e - 1), x)) return false;
+      if (e == 0 && !before(ppos, std::make_pair(k, k), x)) return false;
+      if (e == 0 && k > 0 && !before(rowpos, std::make_tuple(k - 1, j, s, k), x)) return false;
+      for (int i = i0; i < i1; ++i) {
+        if (!before(ppos, std::make_pair(i, k), x)) return false;
+        if (k > 0 && !before(rowpos, std::make_tuple(k - 1, j, s, i), x)) return false;
+      }
+    } else {
+      const int i = it.l, k = it.k;
+      if (i > k && !before(ppos, std::make_pair(i - 1, k), x)) return false;
+      if (k > 0)
+        for (int s = 0; s < ns; ++s)
+          if (!before(rowpos, std::make_tuple(k - 1, k, s, i), x)) return false;
+    }
+  }
+  (void)p; (void)q;
+  return true;
+}
 
 static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp) {
   const int kmax = std::min(p, q), ns = (b + FLOW_SW - 1) / FLOW_SW, ng = b / (b < 32 ? b : 32);
@@ -404,47 +457,6 @@ static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp) {
       }
     }
   }
-  auto valid = [&](const std::vector<Item>& L) {
-    // position of every task; check deps precede
-    std::map<std::tuple<int, int, int, int, int>, int> pos;  // (type, a, b, c, d)
-    for (int x = 0; x < (int)L.size(); ++x) {
-      const Item& it = L[x];
-      int ty = it.ts & 0xff;
-      if (ty == T_CHAIN) pos[std::make_tuple(T_CHAIN, it.k & 0xffff, it.m, (it.ts >> 8) & 0xff, it.k >> 16)] = x;
-      else pos[std::make_tuple(0, it.l, it.k, 0, 0)] = x;
-    }
-    auto seg_of = [&](int k, int j, int i) { return (i - k - 1) / seglen_of(k, j); };
-    for (int x = 0; x < (int)L.size(); ++x) {
-      const Item& it = L[x];
-      int ty = it.ts & 0xff;
-      std::vector<int> deps;
-      if (ty == T_CHAIN) {
-        int s = (it.ts >> 8) & 0xff, k = it.k & 0xffff, e = it.k >> 16, j = it.m, i0 = it.l & 0xffff, i1 = it.l >> 16;
-        if (e > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k, j, s, e - 1)]);
-        else deps.push_back(pos[std::make_tuple(0, k, k, 0, 0)]);
-        if (e == 0 && k > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, j, k))]);
-        for (int i = i0; i < i1; ++i) {
-          deps.push_back(pos[std::make_tuple(0, i, k, 0, 0)]);
-          if (k > 0) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, j, i))]);
-        }
-      } else {
-        int i = it.l, k = it.k;
-        if (i > k) deps.push_back(pos[std::make_tuple(0, i - 1, k, 0, 0)]);
-        if (k > 0)
-          for (int s = 0; s < ns; ++s) deps.push_back(pos[std::make_tuple(T_CHAIN, k - 1, k, s, seg_of(k - 1, k, i))]);
-      }
-      for (int d : deps)
-        if (d >= x) {
-          if (getenv("TQR_DEBUG_PLAN")) {
-            const Item& dd = L[d];
-            fprintf(stderr, "flow plan: task %d (ts=%x l=%x m=%d k=%x) depends on later task %d (ts=%x l=%x m=%d k=%x)\n",
-                    x, it.ts, it.l, it.m, it.k, d, dd.ts, dd.l, dd.m, dd.k);
-          }
-          return false;
-        }
-    }
-    return true;
-  };
   // bump every task's key past its dependencies' keys (tl is topological, step-major), so the
   // estimated-time order is topological by construction
   {
@@ -486,7 +498,7 @@ static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp) {
   });
   fp.items.clear();
   for (auto& t : sorted) fp.items.push_back(t.it);
-  fp.est_order = valid(fp.items);
+  fp.est_order = flow_list_topological(fp.items, p, q, ns);
   if (!fp.est_order) {  // step-major: always topological
     fp.items.clear();
     for (auto& t : tl) fp.items.push_back(t.it);
@@ -548,10 +560,20 @@ static size_t tpimg_doubles(int b) {  // packed T image (Geo<b>::TPIMG)
   const size_t nri = (b < 32 ? b : 32) / 4;
   return (16 * nri * nri + 127) / 128 * 128;
 }
+// fp32 chain image slots (doubles; tiles.hpp Geo32 / Img<B, float>)
+static size_t vimg32_doubles(int b) {
+  const size_t nmi = (b < 32 ? b : 32) / 16;
+  return (size_t)(b / 16) * nmi * 256;  // (VA + VB) floats / 2
+}
+static size_t timg32_doubles(int b) {
+  const size_t nmi = (b < 32 ? b : 32) / 16, npr = nmi * (nmi + 1) / 2;
+  return (npr * 256 / 2 + 127) / 128 * 128;
+}
 // flow engine workspace of one step with `rows` tile rows (flow.hpp flow_vw_off / flow_tw_off)
-static size_t wk_bytes(int b, int rows) {
+static size_t wk_bytes(int b, int rows, int dtype) {
   const size_t ng = b / (b < 32 ? b : 32);
-  return (size_t)rows * ng * (vimg_doubles(b) + tpimg_doubles(b)) * sizeof(double);
+  const size_t slot = dtype == TQR_F64 ? vimg_doubles(b) + tpimg_doubles(b) : vimg32_doubles(b) + timg32_doubles(b);
+  return (size_t)rows * ng * slot * sizeof(double);
 }
 
 }  // namespace tqr
@@ -773,7 +795,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     // one workspace per step k: V then T images of tiles (k..p-1, k), every group
     for (int k = 0; k < pl->kmax; ++k) {
       double* w = nullptr;
-      if (hipMalloc(&w, wk_bytes(b, pl->p - k)) != hipSuccess) { tqr_plan_destroy(pl); return TQR_ENOMEM; }
+      if (hipMalloc(&w, wk_bytes(b, pl->p - k, dtype)) != hipSuccess) { tqr_plan_destroy(pl); return TQR_ENOMEM; }
       pl->wk.push_back(w);
     }
     if (hipMemcpy(pl->d_wk, pl->wk.data(), sizeof(double*) * pl->kmax, hipMemcpyHostToDevice) != hipSuccess) {
@@ -792,7 +814,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
       }
     }
     pl->kflow = resolve_flow(b, dtype);
-    pl->ldsF = lds_flow(b);
+    pl->ldsF = lds_flow(b, dtype);
     int dev = 0;
     hipDeviceProp_t pr;
     if (!pl->kflow || hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&pr, dev) != hipSuccess) {
@@ -949,6 +971,38 @@ int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, in
 }
 
 int tqr_flow_strip_width(void) { return FLOW_SW; }
+
+int tqr_flow_order_check(int M, int N, int b, const int* items, int n) {
+  if (M <= 0 || N <= 0 || !valid_b(b) || !items || n <= 0) return TQR_EINVAL;
+  std::vector<Item> L(n);
+  for (int x = 0; x < n; ++x) L[x] = Item{items[4 * x], items[4 * x + 1], items[4 * x + 2], items[4 * x + 3]};
+  return flow_list_topological(L, M, N, (b + FLOW_SW - 1) / FLOW_SW) ? 1 : 0;
+}
+
+int tqr_plan_set_tasks(tqr_plan* pl, const int* items, int n) {
+  if (!pl || !items || pl->engine != TQR_ENGINE_FLOW || pl->world != 1 || n != pl->nflow) return TQR_EINVAL;
+  std::vector<Item> L(n), cur(n);
+  for (int x = 0; x < n; ++x) L[x] = Item{items[4 * x], items[4 * x + 1], items[4 * x + 2], items[4 * x + 3]};
+  std::lock_guard<std::mutex> lk(pl->mu);
+  HIPCHK(hipEventSynchronize(pl->evDone));  // no execute may be using the current list
+  HIPCHK(hipMemcpy(cur.data(), pl->d_flow, sizeof(Item) * n, hipMemcpyDeviceToHost));
+  auto key = [](const Item& a) { return std::make_tuple(a.ts, a.l, a.m, a.k); };
+  std::vector<std::tuple<int, int, int, int>> ka, kb;
+  for (auto& it : L) ka.push_back(key(it));
+  for (auto& it : cur) kb.push_back(key(it));
+  std::sort(ka.begin(), ka.end());
+  std::sort(kb.begin(), kb.end());
+  if (ka != kb || !flow_list_topological(L, pl->p, pl->q, pl->ns)) return TQR_EINVAL;
+  HIPCHK(hipMemcpy(pl->d_flow, L.data(), sizeof(Item) * n, hipMemcpyHostToDevice));
+  return TQR_OK;
+}
+
+int tqr_plan_debug_workspace(const tqr_plan* pl, int k, void* host, size_t bytes) {
+  if (!pl || pl->engine != TQR_ENGINE_FLOW || k < 0 || k >= pl->kmax || !host) return TQR_EINVAL;
+  const size_t have = wk_bytes(pl->b, pl->p - k, pl->dtype);
+  HIPCHK(hipMemcpy(host, pl->wk[k], std::min(bytes, have), hipMemcpyDeviceToHost));
+  return (int)std::min<size_t>(have, 0x7fffffff);
+}
 
 int tqr_flow_plan_export(int M, int N, int b, int seglen, int* items, int cap) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1) return TQR_EINVAL;

@@ -177,23 +177,22 @@ __device__ __forceinline__ void wg_publish(int* p, int delta, bool sys = false) 
   }
 }
 
-template <int B>
+template <int B, typename S>
 __device__ __forceinline__ size_t flow_vw_off(int p, int i, int k, int g) {
-  using G = Geo<B>;
-  return ((size_t)(i - k) * G::NG + g) * G::VIMG;
+  return ((size_t)(i - k) * Geo<B>::NG + g) * Img<B, S>::V;
 }
-template <int B>
+template <int B, typename S>
 __device__ __forceinline__ size_t flow_tw_off(int p, int i, int k, int g) {
-  using G = Geo<B>;
-  return (size_t)(p - k) * G::NG * G::VIMG + ((size_t)(i - k) * G::NG + g) * G::TPIMG;
+  constexpr int NG = Geo<B>::NG;
+  return (size_t)(p - k) * NG * Img<B, S>::V + ((size_t)(i - k) * NG + g) * Img<B, S>::T;
 }
-template <int B>
+template <int B, typename S>
 __device__ __forceinline__ double* flow_tw(const FlowArgs& a, int i, int k, int g) {
-  return a.Wk[k] + flow_tw_off<B>(a.p, i, k, g);
+  return a.Wk[k] + flow_tw_off<B, S>(a.p, i, k, g);
 }
-template <int B>
+template <int B, typename S>
 __device__ __forceinline__ double* flow_vw(const FlowArgs& a, int i, int k, int g) {
-  return a.Wk[k] + flow_vw_off<B>(a.p, i, k, g);
+  return a.Wk[k] + flow_vw_off<B, S>(a.p, i, k, g);
 }
 
 // ---- LDS-DMA staging of one reflector group ------------------------------------------------
@@ -206,9 +205,10 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 // DMA job of one group for apply_zw's hook: step m issues this wave's m-th LDS-DMA instruction
 // (V image instructions first, then T), so the issue cost hides under the MFMA stream.
-template <int B>
+template <int B, typename S = double>
 struct DmaJob {
-  static constexpr int NIV = Geo<B>::VIMG / 128, NIT = Geo<B>::TPIMG / 128;
+  static constexpr int VIMG = Img<B, S>::V;
+  static constexpr int NIV = Img<B, S>::V / 128, NIT = Img<B, S>::T / 128;
   static constexpr int PV = (NIV + FLOW_NW - 1) / FLOW_NW, PT = (NIT + FLOW_NW - 1) / FLOW_NW;
   static constexpr int STEPS = PV + PT;
   double* dst;
@@ -228,7 +228,7 @@ struct DmaJob {
       dma16(v + u * 128 + 2 * lane, dst + u * 128);
     } else if (m < STEPS) {
       const int u = min(w + FLOW_NW * (m - PV), NIT - 1);
-      dma16(t + u * 128 + 2 * lane, dst + Geo<B>::VIMG + u * 128);
+      dma16(t + u * 128 + 2 * lane, dst + VIMG + u * 128);
     }
   }
   // One wave-wide 16-B-per-lane LDS-DMA (1 KiB, lane-linear at lds_wave). Issued as inline asm:
@@ -368,6 +368,11 @@ __device__ __forceinline__ void st_pair(__amdgpu_buffer_rsrc_t rs, unsigned off,
   }
 }
 
+// the fp32 chain's operand images of one group (chain32.hpp)
+template <int B>
+__device__ __noinline__ void write_images32(const double* Vs, const double* Ts, __amdgpu_buffer_rsrc_t rv,
+                                            __amdgpu_buffer_rsrc_t rt);
+
 // ---- panel tasks ---------------------------------------------------------------------------
 template <int B, typename S>
 __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* lds, int* sflag) {
@@ -470,11 +475,15 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     __syncthreads();
     FST(11);
     {  // V image (explicit) and packed T image of this group for the chains (LDS-DMA sources)
-      double* tg = flow_tw<B>(a, qrs ? k : l, k, g);
-      double* vg = flow_vw<B>(a, qrs ? k : l, k, g);
+      double* tg = flow_tw<B, S>(a, qrs ? k : l, k, g);
+      double* vg = flow_vw<B, S>(a, qrs ? k : l, k, g);
       const __amdgpu_buffer_rsrc_t rv = uniform_rsrc(vg), rt = uniform_rsrc(tg);
-      for (int idx = t; idx < G::TPIMG / 2; idx += FLOW_NT) st_pair<double>(rt, 16 * idx, Tp[2 * idx], Tp[2 * idx + 1]);
-      for (int idx = t; idx < G::VSZ / 2; idx += FLOW_NT) st_pair<double>(rv, 16 * idx, Vs[2 * idx], Vs[2 * idx + 1]);
+      if constexpr (sizeof(S) == 8) {
+        for (int idx = t; idx < G::TPIMG / 2; idx += FLOW_NT) st_pair<double>(rt, 16 * idx, Tp[2 * idx], Tp[2 * idx + 1]);
+        for (int idx = t; idx < G::VSZ / 2; idx += FLOW_NT) st_pair<double>(rv, 16 * idx, Vs[2 * idx], Vs[2 * idx + 1]);
+      } else {
+        write_images32<B>(Vs, Ts, rv, rt);  // the fp32 chain's operand images (chain32.hpp)
+      }
     }
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
     wg_publish(&a.Rc[(size_t)k * NG + g], 1);
@@ -525,7 +534,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
 // then LDS-DMA the images from their own HBM exactly as the owner's chains do. Per-member flags
 // (not counters) let the forwards of different members run concurrently on different
 // workgroups: a panel's images leave as fast as they are produced.
-template <int B>
+template <int B, typename S>
 __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sflag) {
   using G = Geo<B>;
   constexpr int NG = G::NG;
@@ -534,15 +543,15 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
     bool ok = true;
     if (t == 0) ok = spin_ge(&a.Rc[(size_t)k * NG + g], pos + 1, a.err);
     if (!wg_verdict(ok, sflag)) return;
-    const size_t vo = flow_vw_off<B>(a.p, i, k, g), to = flow_tw_off<B>(a.p, i, k, g);
+    const size_t vo = flow_vw_off<B, S>(a.p, i, k, g), to = flow_tw_off<B, S>(a.p, i, k, g);
     const __amdgpu_buffer_rsrc_t vsrc = uniform_rsrc(a.Wk[k] + vo), tsrc = uniform_rsrc(a.Wk[k] + to);
     for (int r = 0; r < a.world; ++r) {
       if (r == a.rank) continue;
       double* pw = a.peers[r].Wk[k];
       const __amdgpu_buffer_rsrc_t vdst = uniform_rsrc(pw + vo), tdst = uniform_rsrc(pw + to);
-      for (int c = t; c < G::VIMG / 2; c += FLOW_NT)
+      for (int c = t; c < Img<B, S>::V / 2; c += FLOW_NT)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(vsrc, 16 * c, 0, 16), vdst, 16 * c, 0, 17);
-      for (int c = t; c < G::TPIMG / 2; c += FLOW_NT)
+      for (int c = t; c < Img<B, S>::T / 2; c += FLOW_NT)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(tsrc, 16 * c, 0, 16), tdst, 16 * c, 0, 17);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -606,8 +615,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   const int P = uni(a.p), Q = uni(a.q), NS = uni(a.ns);
   int* const err = uni(a.err);
   int* const Tc = uni(a.Tc);
-  auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B>(P, i_, k, g_); };
-  auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B>(P, i_, k, g_); };
+  auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B, S>(P, i_, k, g_); };
+  auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B, S>(P, i_, k, g_); };
   int* const rc = &a.Rc[(size_t)k * NG];
   int* const acg = &a.Ac[(((size_t)k * Q + j) * NS + s) * NG];  // per head-row group
   auto tc = [&](int i) { return &Tc[((size_t)i * Q + j) * NS + s]; };
@@ -796,19 +805,23 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   FST(4);
 }
 
-// dynamic LDS (doubles) of the two task paths; two ints follow (task index, wait verdict)
-template <int B>
+}  // namespace tqr
+#include "chain32.hpp"
+namespace tqr {
+
+// dynamic LDS (doubles) of the task paths; the LDS tail (task word, verdicts, ...) follows
+template <int B, typename S>
 constexpr int flow_lds_doubles() {
   using G = Geo<B>;
   constexpr int panel = G::VSZ + 8 * G::TSZ + G::IB + 2 + 2 * 4 * 32 + 4 * 32 + 2 * 32;
-  constexpr int chain = 2 * (G::VIMG + G::TPIMG);
+  constexpr int chain = 2 * (Img<B, S>::V + Img<B, S>::T);
   return panel > chain ? panel : chain;
 }
 
 template <int B, typename S>
 __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
   extern __shared__ __align__(16) double lds[];
-  int* s_task = reinterpret_cast<int*>(lds + flow_lds_doubles<B>());
+  int* s_task = reinterpret_cast<int*>(lds + flow_lds_doubles<B, S>());
   int* s_flag = s_task + 1;
 #ifdef TQR_FLOW_STAMPS
   if (threadIdx.x == 0) {
@@ -837,10 +850,14 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
     }
 #endif
     if (type == T_CHAIN) {
-      flow_chain<B, S>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
-                       s_flag);
+      if constexpr (sizeof(S) == 8)
+        flow_chain<B, S>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
+                         s_flag);
+      else
+        flow_chain32<B>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
+                        s_flag);
     } else if (type == T_FWD) {
-      flow_fwd<B>(a, it.l, it.k, s_flag);
+      flow_fwd<B, S>(a, it.l, it.k, s_flag);
     } else {
       flow_panel<B, S>(a, type, it.l, it.k, lds, s_flag);
     }

@@ -80,6 +80,28 @@ struct Geo {
   __device__ static constexpr int pc(int c) { return (c & 3) * NRI + (c >> 2); }
 };
 
+// fp32 chain geometry (chain32.hpp): v_mfma_f32_16x16x4_f32 tiles of 16 strip rows (NMT per tile)
+// and 16 reflectors (NMI per group). LDS / workspace images (floats, lane-major 16-B chunks):
+//   VA [mt][chunk < NMI][lane][4]  phase-1 A operands  V[16mt + 4x + r][16mi + y]
+//   VB [mt][wi  < NMI][lane][4]    phase-2 A operands  V[16mt + y][16wi + 4x + r]
+//   TP [pair (mi <= wi)][lane][4]  W = -T^T Z operands -T[16mi + 4x + r][16wi + y]
+// (lane = 16x + y; chunk of VA = (4r + ... see chain32.hpp); slots in doubles, whole KiB.
+template <int B>
+struct Geo32 {
+  static constexpr int IB = Geo<B>::IB, NG = Geo<B>::NG;
+  static constexpr int NMT = B / 16, NMI = IB / 16, NPR = NMI * (NMI + 1) / 2;
+  static constexpr int VA = NMT * NMI * 256, VB = VA, TP = NPR * 256;  // floats
+  static constexpr int VIMG = (VA + VB) / 2;                           // doubles (multiple of 128)
+  static constexpr int TIMG = (TP / 2 + 127) / 128 * 128;
+};
+// workspace slot sizes (doubles) of one reflector group's images, by storage type: fp64 storage
+// = the fp64 chain's V image + packed T; fp32 storage = the fp32 chain's VA/VB/TP images
+template <int B, typename S>
+struct Img {
+  static constexpr int V = sizeof(S) == 8 ? Geo<B>::VIMG : Geo32<B>::VIMG;
+  static constexpr int T = sizeof(S) == 8 ? Geo<B>::TPIMG : Geo32<B>::TIMG;
+};
+
 template <typename S>
 __device__ __forceinline__ double ld(const S* p) { return (double)*p; }
 // L1-bypassing (sc1) load: data handed over by another workgroup inside a launch, read without an

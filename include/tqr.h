@@ -85,6 +85,16 @@ int tqr_flow_strip_width(void);
  * {type | strip << 8, l, m, k} (chains: type 4, l = i0 | i1 << 16, k = step | segment << 16);
  * returns the number of tasks (writes at most `cap`). */
 int tqr_flow_plan_export(int M, int N, int b, int seglen, int* items, int cap);
+/* Replace the persistent engine's task order (the same tasks as the plan's list, 4 ints each as
+ * tqr_flow_plan_export gives them, e.g. from an offline list scheduler): rejected with
+ * TQR_EINVAL unless it is a permutation of the plan's tasks that is topological for every
+ * in-task wait (the engine's deadlock-freedom condition). Single-GPU flow plans only. */
+int tqr_plan_set_tasks(tqr_plan* plan, const int* items, int n);
+/* Host-only: 1 if `items` is topological for the engine's waits on an M x N tile grid, else 0. */
+int tqr_flow_order_check(int M, int N, int b, const int* items, int n);
+/* Diagnostics: copy the persistent engine's panel workspace of step k (the reflector groups'
+ * operand images, DESIGN.md "Data layout") to host memory; returns its size in bytes. */
+int tqr_plan_debug_workspace(const tqr_plan* plan, int k, void* host, size_t bytes);
 
 /* Per-launch statistics of the last execute (filled when the plan was created with
  * tqr_plan_set_profile(plan, 1)): number of kernel launches and the summed device time of
