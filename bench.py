@@ -227,6 +227,26 @@ def main():
         el = float(tt.item())
     plan.status(stream)
     ok_rel = check_output(A0, A, m, n) if world == 1 else None
+    dist_info = None
+    if dist:
+        # per rank: engine status (raised above if not ok), forwarded bytes, and with a stamps build
+        # (TQR_LIB=libtqr_fst.so) the share of workgroup time the forward tasks took
+        mine = {"rank": rank, "status": "ok", "fwd_bytes": plan.fwd_bytes()}
+        L = tqr.lib()
+        if hasattr(L, "tqr_debug_flow_stamps"):
+            import ctypes
+            nc = L.tqr_debug_flow_stamp_count()
+            grid = ctypes.c_int()
+            L.tqr_plan_info(plan.h, None, None, None, ctypes.byref(grid))
+            stv = (ctypes.c_ulonglong * (nc * grid.value))()
+            if L.tqr_debug_flow_stamps(stv, grid.value) == 0:
+                tot = sum(stv)
+                fwd = sum(stv[w * nc + 23] for w in range(grid.value))
+                mine["fwd_share_of_wg_time"] = round(fwd / tot, 4) if tot else None
+                mine["fwd_ms_per_wg"] = round(fwd / grid.value / 1e5, 3)  # s_memrealtime at 100 MHz
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        dist_info = {"world_size": world, "ranks": ranks}
     ms_step = el / args.steps * 1e3
     total_flops = qr_flops(m, n) * args.steps
     value = total_flops / el / 1e9
@@ -289,6 +309,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "check": {"column_norm_rel_err": ok_rel} if ok_rel is not None else None,
+            "dist": dist_info,
         }
         print(json.dumps(line))
     if dist:

@@ -951,6 +951,15 @@ int tqr_dist_reset(tqr_plan* pl, void* stream) {
   return TQR_OK;
 }
 
+long long tqr_plan_fwd_bytes(const tqr_plan* pl) {
+  if (!pl) return TQR_EINVAL;
+  if (pl->world < 2) return 0;
+  long long members = 0;  // panel members of the tile columns this rank owns
+  for (int k = pl->rank; k < pl->kmax; k += pl->world) members += pl->p - k;
+  const long long slot = (long long)(wk_bytes(pl->b, 1, pl->dtype));  // one member's images, all groups
+  return members * slot * (pl->world - 1);
+}
+
 int tqr_dist_owner(const tqr_plan* pl, int tile_col) {
   if (!pl || tile_col < 0 || tile_col >= pl->q) return TQR_EINVAL;
   return tile_col % pl->world;
@@ -1431,6 +1440,7 @@ extern "C" int tqr_debug_stamps(unsigned long long* out, int reset) {
 #endif
 
 #ifdef TQR_FLOW_STAMPS
+extern "C" int tqr_debug_flow_stamp_count(void) { return FST_N; }
 // per-workgroup activity sums of the last k_flow launch (FST_N categories, flow.hpp FST)
 extern "C" int tqr_debug_flow_stamps(unsigned long long* out, int nblocks) {
   if (nblocks > 4096) return TQR_EINVAL;

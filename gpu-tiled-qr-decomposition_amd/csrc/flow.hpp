@@ -48,8 +48,9 @@ constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel memb
 // start (lookahead column j = k+1 / other columns), 20 chain Rc waits inside a lookahead-column
 // element (0 is then the same for other columns), 21 / 22 chain drain of the wave's own memory
 // operations before the group's polls, groups > 0 / group 0 (stamps build only; at group 0 this
-// includes the element's strip loads, which the real kernel overlaps with phase 1).
-constexpr int FST_N = 23;
+// includes the element's strip loads, which the real kernel overlaps with phase 1), 23 forward
+// tasks (multi-GPU: panel images copied to the peers, including their waits for the panel).
+constexpr int FST_N = 24;
 #ifdef TQR_FLOW_STAMPS
 extern __device__ unsigned long long g_fst[];
 extern __device__ unsigned long long g_ttl[];  // per task: start, end (s_memrealtime), workgroup
@@ -564,6 +565,7 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
     }
     __syncthreads();
   }
+  FST(23);
 }
 
 // ---- chain tasks ---------------------------------------------------------------------------

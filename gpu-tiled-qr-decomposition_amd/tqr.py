@@ -17,7 +17,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtqr.so")
+# TQR_LIB: a diagnostic build of the same library (e.g. libtqr_fst.so, activity stamps) by file name
+LIB_PATH = os.path.join(HERE, os.environ.get("TQR_LIB", "libtqr.so"))
 
 TQR_F32, TQR_F64 = 0, 1
 QRS, SAPP, QRD, DAPP = 0, 1, 2, 3
@@ -220,6 +221,11 @@ class DistTiledQR(TiledQR):
 
     def owns(self, tile_col):
         return tile_col % self.world == self.rank
+
+    def fwd_bytes(self):
+        """Bytes this rank forwards to its peers per factorisation (panel V/T images over xGMI)."""
+        lib().tqr_plan_fwd_bytes.restype = ctypes.c_longlong
+        return int(lib().tqr_plan_fwd_bytes(self.h))
 
     def execute(self, A, tau, ldda=None, stream=None):
         """Reset this rank's counters, barrier over all ranks, launch (stream-ordered)."""

@@ -123,6 +123,9 @@ int tqr_dist_export(tqr_plan* plan, void* handles, size_t len);
 int tqr_dist_import(tqr_plan* plan, const void* all_handles, size_t len);
 int tqr_dist_reset(tqr_plan* plan, void* stream);
 int tqr_dist_owner(const tqr_plan* plan, int tile_col);
+/* bytes this rank forwards to its peers per factorisation (every owned panel member's V/T images,
+ * all reflector groups, to each of the world - 1 peers); 0 for a single-GPU plan */
+long long tqr_plan_fwd_bytes(const tqr_plan* plan);
 /* host-only: this rank's task-list length and number of forward tasks */
 int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd);
 

@@ -20,13 +20,13 @@ for rep in range(2):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
 nb = torch.cuda.get_device_properties(0).multi_processor_count
-NC = 23
+NC = 24
 st = (ctypes.c_ulonglong * (NC * nb))()
 assert L.tqr_debug_flow_stamps(st, nb) == 0
 names = ["chain Rc wait in-elem other", "panel waits", "chain head-row store", "chain phase 1 Z (+DMA)",
          "chain strip I/O+publish", "panel_factor", "dequeue/dispatch/exit", "chain drain+barrier",
          "chain Tc waits", "chain Ac waits", "panel I/O+images", "panel build_t", "panel trail MFMA+publish", "chain phase 2", "chain next-head load", "chain W + head update", "panel trail loads", "panel trail stores",
-         "chain Rc wait @start la-col", "chain Rc wait @start other", "chain Rc wait in-elem la-col", "chain own-memory drain @group>0", "chain own-memory drain @group0"]
+         "chain Rc wait @start la-col", "chain Rc wait @start other", "chain Rc wait in-elem la-col", "chain own-memory drain @group>0", "chain own-memory drain @group0", "fwd tasks (multi-GPU)"]
 tot = [sum(st[w * NC + c] for w in range(nb)) for c in range(NC)]
 allt = sum(tot)
 print(f"{m}x{n} b={b}: wall {ms:.1f} ms; {nb} workgroups; sum of stamps {allt / nb / 1e5:.1f} ms per WG")
