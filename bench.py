@@ -165,6 +165,8 @@ def main():
                     help="matrix element type: f64 (fp64 MFMA chains) or f32 (fp32 MFMA chains, fp64 panel "
                          "factorisation; BASELINE configs[4])")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-api", action="store_true",
+                    help="skip the PCIe-inclusive host-pointer timing (tqr_*geqrt_host)")
     ap.add_argument("--cpu-sample", type=int, default=6144)
     args = ap.parse_args()
 
@@ -282,6 +284,24 @@ def main():
         "panel_kernel_ms_total": round(st["ms_panel"], 3),
         "whole_factorisation_frac_of_peak": round(value / 1e3 / (world * peak), 4),
     }
+    host_api = None
+    if world == 1 and not args.no_host_api:
+        # the reference's calling convention (host matrix in, factorised host matrix out): pageable
+        # host array -> pinned staging -> HBM, factorisation, and back (outside the timed region;
+        # reported beside, never as, the value)
+        Ah = A0.cpu().numpy()
+        times = []
+        for _ in range(2):
+            F = Ah.copy()
+            t0 = time.perf_counter()
+            tqr.geqrt_host(F, b)
+            times.append(time.perf_counter() - t0)
+        th = min(times)
+        host_api = {"ms": round(th * 1e3, 1), "gflops": round(qr_flops(m, n) / th / 1e9, 1),
+                    "h2d_d2h_bytes": 2 * Ah.nbytes,
+                    "note": "tqr_geqrt_host end to end: pageable host array, pinned double-buffered staging, "
+                            "async copies, factorisation, copies back, tau expanded to m x n"}
+        del Ah, F
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample, 256)
@@ -310,6 +330,7 @@ def main():
             "cpu_baseline": cpu,
             "check": {"column_norm_rel_err": ok_rel} if ok_rel is not None else None,
             "dist": dist_info,
+            "host_api": host_api,
         }
         print(json.dumps(line))
     if dist:

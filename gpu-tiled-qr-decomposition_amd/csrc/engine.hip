@@ -14,7 +14,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
+#include <thread>
 #include <mutex>
 #include <new>
 #include <tuple>
@@ -620,6 +622,15 @@ struct tqr_plan {
   // mutex around each enqueue sequence, and every execute's stream waits for the previous one
   std::mutex mu;
   hipEvent_t evDone = nullptr;
+  // host-pointer path (geqrt_host): device buffers and two pinned staging buffers, kept with the
+  // (cached) plan; hmu serialises whole host-API calls on one plan
+  std::mutex hmu;
+  void* hA = nullptr;
+  void* hT = nullptr;
+  void* pin[2] = {nullptr, nullptr};
+  size_t pin_bytes = 0;
+  hipStream_t sC = nullptr;
+  hipEvent_t pev[2] = {nullptr, nullptr};
 };
 
 #define HIPCHK(x)                                                                         \
@@ -682,6 +693,13 @@ void tqr_plan_destroy(tqr_plan* pl) {
   if (pl->ev0) (void)hipEventDestroy(pl->ev0);
   if (pl->ev1) (void)hipEventDestroy(pl->ev1);
   if (pl->evDone) (void)hipEventDestroy(pl->evDone);
+  if (pl->hA) (void)hipFree(pl->hA);
+  if (pl->hT) (void)hipFree(pl->hT);
+  for (int x = 0; x < 2; ++x) {
+    if (pl->pin[x]) (void)hipHostFree(pl->pin[x]);
+    if (pl->pev[x]) (void)hipEventDestroy(pl->pev[x]);
+  }
+  if (pl->sC) (void)hipStreamDestroy(pl->sC);
   for (auto e : pl->prof_ev) (void)hipEventDestroy(e);
   close_opened(pl);
   if (pl->d_peers) (void)hipFree(pl->d_peers);
@@ -1181,36 +1199,108 @@ int tqr_sgeqrt_tiled(int m, int n, int b, float* dA, int ldda, float* dtau, void
   return st ? st : tqr_plan_execute(pl, dA, ldda, dtau, stream);
 }
 
-// Host-pointer factorisation: 2-D copies in, factorise, copies out, tau expanded to the
-// reference's m x n layout (column k*b of tau = compact column k).
+// Host-pointer factorisation (the reference's calling convention: cudaQRTask copies a host matrix
+// in and out, gpucalc.cu:1614-1619, 1665-1670 — one cudaMemcpy per column). Here the transfers go
+// through two pinned staging buffers of the (cached) plan: the host copies column blocks into one
+// while the DMA engine moves the other (hipMemcpyAsync on the plan's copy stream), the factorisation
+// is stream-ordered behind the last upload, and the results come back the same way. The device
+// buffers stay with the plan (no allocation per call). tau is expanded to the reference's m x n
+// layout (column k*b of tau = compact column k).
+static constexpr size_t kPinBytes = 64ull << 20;
+static int host_staging(tqr_plan* pl, size_t es) {
+  if (pl->hA) return TQR_OK;
+  const size_t abytes = es * (size_t)pl->m * pl->n, tbytes = es * (size_t)pl->m * pl->kmax;
+  pl->pin_bytes = std::min(kPinBytes, std::max(abytes, tbytes));
+  if (hipMalloc(&pl->hA, abytes) != hipSuccess || hipMalloc(&pl->hT, tbytes) != hipSuccess) return TQR_ENOMEM;
+  for (int x = 0; x < 2; ++x) {
+    if (hipHostMalloc(&pl->pin[x], pl->pin_bytes, hipHostMallocDefault) != hipSuccess) return TQR_ENOMEM;
+    if (hipEventCreateWithFlags(&pl->pev[x], hipEventDisableTiming) != hipSuccess) return TQR_EHIP;
+  }
+  if (hipStreamCreateWithFlags(&pl->sC, hipStreamNonBlocking) != hipSuccess) return TQR_EHIP;
+  return TQR_OK;
+}
+
+// host-side column copies of one staging chunk, split over a few threads (one thread moves
+// ~10 GB/s; the pinned DMA runs at PCIe rate)
+static void par_columns(size_t nc, const std::function<void(size_t)>& f) {
+  const size_t nt = std::min<size_t>({nc, 8, std::max(1u, std::thread::hardware_concurrency())});
+  if (nt <= 1) {
+    for (size_t j = 0; j < nc; ++j) f(j);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (size_t j = t; j < nc; j += nt) f(j);
+    });
+  for (auto& x : th) x.join();
+}
+
+// copy `ncols` columns of `rows` elements between strided host memory (ld) and packed device memory
+// through the pinned buffers, double-buffered
+static int staged_copy(tqr_plan* pl, char* host, size_t ld, char* dev, size_t rows, size_t ncols, size_t es, bool h2d) {
+  const size_t col = es * rows, per = std::max<size_t>(1, pl->pin_bytes / col);
+  const size_t nchunk = (ncols + per - 1) / per;
+  auto chunk = [&](size_t c, size_t& c0, size_t& nc) { c0 = c * per; nc = std::min(per, ncols - c0); };
+  if (h2d) {
+    for (size_t c = 0; c < nchunk; ++c) {
+      size_t c0, nc;
+      chunk(c, c0, nc);
+      char* pb = (char*)pl->pin[c & 1];
+      HIPCHK(hipEventSynchronize(pl->pev[c & 1]));  // the DMA from this buffer two chunks ago is done
+      par_columns(nc, [&](size_t j) { memcpy(pb + j * col, host + (c0 + j) * ld * es, col); });
+      HIPCHK(hipMemcpyAsync(dev + c0 * col, pb, nc * col, hipMemcpyHostToDevice, pl->sC));
+      HIPCHK(hipEventRecord(pl->pev[c & 1], pl->sC));
+    }
+    return TQR_OK;
+  }
+  auto issue = [&](size_t c) -> int {
+    size_t c0, nc;
+    chunk(c, c0, nc);
+    HIPCHK(hipMemcpyAsync(pl->pin[c & 1], dev + c0 * col, nc * col, hipMemcpyDeviceToHost, pl->sC));
+    HIPCHK(hipEventRecord(pl->pev[c & 1], pl->sC));
+    return TQR_OK;
+  };
+  for (size_t c = 0; c < std::min<size_t>(2, nchunk); ++c)
+    if (int st = issue(c)) return st;
+  for (size_t c = 0; c < nchunk; ++c) {
+    size_t c0, nc;
+    chunk(c, c0, nc);
+    HIPCHK(hipEventSynchronize(pl->pev[c & 1]));
+    const char* pb = (const char*)pl->pin[c & 1];
+    par_columns(nc, [&](size_t j) { memcpy(host + (c0 + j) * ld * es, pb + j * col, col); });
+    if (c + 2 < nchunk)
+      if (int st = issue(c + 2)) return st;
+  }
+  return TQR_OK;
+}
+
 static int geqrt_host(void* A, void* tau, int m, int n, int ldm, int b, int dtype, int engine = TQR_ENGINE_DEFAULT) {
   if (!A || ldm < m || !valid_b(b) || m <= 0 || n <= 0 || m % b || n % b) return TQR_EINVAL;
   tqr_plan* pl;
   int st = cached_plan(m, n, b, dtype, &pl, engine);
   if (st) return st;
-  size_t es = dtype == TQR_F64 ? 8 : 4;
-  void *dA = nullptr, *dT = nullptr;
-  int kmax = std::min(m, n) / b;
-  if (hipMalloc(&dA, es * (size_t)m * n) != hipSuccess) return TQR_ENOMEM;
-  if (hipMalloc(&dT, es * (size_t)m * kmax) != hipSuccess) { (void)hipFree(dA); return TQR_ENOMEM; }
-  st = TQR_OK;
-  if (hipMemcpy2D(dA, es * m, A, es * ldm, es * m, n, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(dT, 0, es * (size_t)m * kmax) != hipSuccess) st = TQR_EHIP;
-  if (!st) st = tqr_plan_execute(pl, dA, m, dT, nullptr);
-  if (!st && hipDeviceSynchronize() != hipSuccess) st = TQR_EHIP;
-  if (!st) st = tqr_plan_status(pl, nullptr);
-  if (!st && hipMemcpy2D(A, es * ldm, dA, es * m, es * m, n, hipMemcpyDeviceToHost) != hipSuccess) st = TQR_EHIP;
-  if (!st && tau) {
-    // column k of the compact array -> column k*b of the reference tau matrix, rows k*b..m-1
-    for (int k = 0; k < kmax && !st; ++k) {
-      char* dst = (char*)tau + es * ((size_t)k * b * ldm + (size_t)k * b);
-      const char* src = (const char*)dT + es * ((size_t)k * m + (size_t)k * b);
-      if (hipMemcpy(dst, src, es * (size_t)(m - k * b), hipMemcpyDeviceToHost) != hipSuccess) st = TQR_EHIP;
-    }
+  std::lock_guard<std::mutex> lk(pl->hmu);
+  const size_t es = dtype == TQR_F64 ? 8 : 4;
+  const int kmax = std::min(m, n) / b;
+  if ((st = host_staging(pl, es))) return st;
+  char* dA = (char*)pl->hA;
+  char* dT = (char*)pl->hT;
+  if ((st = staged_copy(pl, (char*)A, ldm, dA, m, n, es, true))) return st;
+  HIPCHK(hipMemsetAsync(dT, 0, es * (size_t)m * kmax, pl->sC));
+  if ((st = tqr_plan_execute(pl, dA, m, dT, pl->sC))) return st;
+  if ((st = tqr_plan_status(pl, pl->sC))) return st;
+  if ((st = staged_copy(pl, (char*)A, ldm, dA, m, n, es, false))) return st;
+  if (tau) {
+    // compact tau (m x kmax, packed) -> the reference's m x n matrix: column k of the compact
+    // array is column k*b of tau, rows k*b .. m-1
+    std::vector<char> ct(es * (size_t)m * kmax);
+    if ((st = staged_copy(pl, ct.data(), m, dT, m, kmax, es, false))) return st;
+    for (int k = 0; k < kmax; ++k)
+      memcpy((char*)tau + es * ((size_t)k * b * ldm + (size_t)k * b), ct.data() + es * ((size_t)k * m + (size_t)k * b),
+             es * (size_t)(m - k * b));
   }
-  (void)hipFree(dA);
-  (void)hipFree(dT);
-  return st;
+  return TQR_OK;
 }
 
 int tqr_dgeqrt_host(double* A, double* tau, int m, int n, int ldm, int b) { return geqrt_host(A, tau, m, n, ldm, b, TQR_F64); }
