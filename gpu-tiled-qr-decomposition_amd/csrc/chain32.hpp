@@ -99,11 +99,43 @@ __device__ __forceinline__ void ld_chunks(float (&a)[4 * N], const float* img, i
   }
 }
 
+// Phase-2 hook: nothing after the strip tiles are final (every group but an element's last)
+struct NoPost32 {
+  template <int N>
+  __device__ __forceinline__ void at(int, f4v (&)[N]) const {}
+  template <int N>
+  __device__ __forceinline__ void fin(f4v (&)[N]) const {}
+};
+// Element hand-over inside the last group's phase 2: once tile pair p of the strip is final (its
+// MFMAs issued one pair earlier), it is stored (write-through) and the same registers start
+// loading pair p of the next element's strip — the element boundary no longer waits for 128 KiB
+// of strip out and in per workgroup (what-if without strip I/O: -71 ms at 32768^2 fp32).
+template <int B>
+struct XPipe32 {
+  __amdgpu_buffer_rsrc_t out, in;  // this element's strip / the next element's (same columns)
+  unsigned base;
+  __device__ __forceinline__ void xfer(int mt, f4v (&X)[Geo32<B>::NMT]) const {
+    st_f4(out, base + 64u * mt, X[mt]);
+    X[mt] = ld_f4(in, base + 64u * mt);
+  }
+  __device__ __forceinline__ void at(int mt, f4v (&X)[Geo32<B>::NMT]) const {
+    if (mt >= 2) {
+      xfer(mt - 2, X);
+      xfer(mt - 1, X);
+    }
+  }
+  __device__ __forceinline__ void fin(f4v (&X)[Geo32<B>::NMT]) const {
+    if constexpr (Geo32<B>::NMT >= 2) xfer(Geo32<B>::NMT - 2, X);
+    xfer(Geo32<B>::NMT - 1, X);
+  }
+};
+
 // One reflector group applied to a strip (X) with head accumulator Hg (TS) or none (GE, UNMQR:
-// the strip is the head tile itself). Phase 1 carries the hook (next group's LDS-DMA).
-template <int B, bool TS, typename Hook>
+// the strip is the head tile itself). Phase 1 carries the hook (next group's LDS-DMA), phase 2
+// the post hook (element hand-over).
+template <int B, bool TS, typename Hook, typename Post = NoPost32>
 __device__ __forceinline__ void apply32(const float* VA, const float* VB, const float* TPi, f4v (&X)[Geo32<B>::NMT],
-                                        f4v (&Hg)[Geo32<B>::NMT], const Hook& hook) {
+                                        f4v (&Hg)[Geo32<B>::NMT], const Hook& hook, const Post& post = Post()) {
   using G32 = Geo32<B>;
   constexpr int NMT = G32::NMT, NMI = G32::NMI;
   const int lane = threadIdx.x & 63;
@@ -161,7 +193,9 @@ __device__ __forceinline__ void apply32(const float* VA, const float* VB, const 
         X[mt] = mfma16(b0[4 * wi + r], W[wi][r], X[mt]);
         if (mt + 1 < NMT) X[mt + 1] = mfma16(b1[4 * wi + r], W[wi][r], X[mt + 1]);
       }
+    post.at(mt, X);  // the previous pair, behind this pair's MFMAs
   }
+  post.fin(X);
 }
 
 // Strip / head tile I/O: tile mt of the strip at column col0 + y, rows 16mt + 4x .. + 3.
@@ -205,7 +239,8 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
   bool dma_next = false;
   PanelView<NG> pv;
   pv.init(sflag + 48);
-  int tc_pf = -1;
+  int tc_pf = -1;     // thread 0: Tc of the next element's tile, loaded two groups ahead
+  bool xin = false;  // this element's strip was loaded during the previous element's last phase 2
   const bool remote = a.dist && (k % a.world != a.rank);
   int* const rf = a.Rf + (size_t)k * P * NG;
   int* fl_pf = nullptr;
@@ -245,8 +280,11 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
     const Strip32<B> xs(Xt, ldm, col);
     if (active) {
       if (ts) {
+#ifndef TQR_DIAG_NOSTRIP
+        if (!xin)
 #pragma unroll
-        for (int mt = 0; mt < NMT; ++mt) X[mt] = ld_f4(xs.rs, xs.off(mt));
+          for (int mt = 0; mt < NMT; ++mt) X[mt] = ld_f4(xs.rs, xs.off(mt));
+#endif
         if (head_in)
 #pragma unroll
           for (int mi = 0; mi < NMI; ++mi) Hd[mi] = ld_f4(hs.rs, hs.off(mi));
@@ -262,6 +300,15 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
       for (int g = 0; g < NG; ++g) {
         {
           bool ok = true;
+          if (t == 0 && g + 1 == NG) {
+            // last group: may the next element's strip stream in during this phase 2? (its tile
+            // must have received step k-1: Tc, loaded two groups ahead)
+#ifdef TQR_DIAG_NOSTRIP
+            sflag[44] = 0;
+#else
+            sflag[44] = (NG > 1 && ts && has_next && (k == 0 || tc_pf >= k)) ? 1 : 0;
+#endif
+          }
           if (t == 0) {
             if (head_in && g + 1 < NG) ok = spin_ge(&acg[g + 1], seg, err);  // head rows of g+1 final
             if (ok) {
@@ -284,7 +331,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
             fl_pf = g + 1 < NG ? rf + (size_t)i * NG + g + 1 : has_next ? rf + (size_t)inext * NG : nullptr;
             fl_pv = fl_pf ? ld_sys(fl_pf) : 0;
           }
-          if (g + 1 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
+          if (g + 2 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
         }
         FST(7);
         const float* img = reinterpret_cast<const float*>(lds + buf * BUF);
@@ -294,13 +341,32 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
         const int gd = g + 1 < NG ? g + 1 : has_next ? 0 : g, id = g + 1 < NG ? i : has_next ? inext : i;
         DmaJob<B, float> d{lds + (buf ^ 1) * BUF, vimg(id, gd), timg(id, gd), sflag};
         dma_next = g + 1 == NG && has_next;
+#if defined(TQR_DIAG_DMA_FIXED)  // what-if: every DMA reads one L2-hot image (results wrong)
+        d.v = vimg(k, 0);
+        d.t = timg(k, 0);
+#endif
+#ifdef TQR_DIAG_NODMA  // what-if: no staging at all (results wrong)
+        const NoHook dh{};
+#else
+        const DmaJob<B, float>& dh = d;
+#endif
+        // (written before the sync; wave-uniform: a scalar branch around the hooked phase 2 — as a
+        // per-lane value the two apply32 bodies became exec-masked twins, and at NG == 1 that
+        // broke the non-hooked one)
+        const bool pipe = NG > 1 && g + 1 == NG && uni(*(volatile int*)(sflag + 44)) != 0;
         if (active) {
           if (ts) {
             // next group's head rows (first element of a later segment) ride this group
             if (head_in && g + 1 < NG)
 #pragma unroll
               for (int mi = 0; mi < NMI; ++mi) Hd[NMI + mi] = ld_f4(hs.rs, hs.off((g + 1) * NMI + mi));
-            apply32<B, true>(VA, VB, TPi, X, Hd, d);
+            if (pipe) {
+              float* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
+              const XPipe32<B> xp{xs.rs, uniform_rsrc(Xn + (size_t)col * ldm), xs.base};
+              apply32<B, true>(VA, VB, TPi, X, Hd, dh, xp);
+            } else {
+              apply32<B, true>(VA, VB, TPi, X, Hd, dh);
+            }
             FST(13);
             if (!has_next)  // segment's last element: the group's head rows leave (write-through)
 #pragma unroll
@@ -315,12 +381,13 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
             for (int mi = 0; mi < NMI; ++mi) Hd[NMT - NMI + mi] = tmp[mi];
             FST(2);
           } else {
-            apply32<B, false>(VA, VB, TPi, Hd, Hd, d);
+            apply32<B, false>(VA, VB, TPi, Hd, Hd, dh);
             FST(13);
           }
         } else {
           for (int m = 0; m < DmaJob<B, float>::STEPS; ++m) d.step(m);
         }
+        if (g + 1 == NG) xin = pipe;
         buf ^= 1;
       }
       return true;
@@ -328,8 +395,11 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
     if (!groups()) return;
     if (active) {
       if (ts) {
+#ifndef TQR_DIAG_NOSTRIP
+        if (!xin)
 #pragma unroll
-        for (int mt = 0; mt < NMT; ++mt) st_f4(xs.rs, xs.off(mt), X[mt]);
+          for (int mt = 0; mt < NMT; ++mt) st_f4(xs.rs, xs.off(mt), X[mt]);
+#endif
       } else if (!has_next) {  // a lone UNMQR (last step): its head tile strip is the result
 #pragma unroll
         for (int mt = 0; mt < NMT; ++mt) st_f4(hs.rs, hs.off(mt), Hd[mt]);

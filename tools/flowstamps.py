@@ -9,9 +9,10 @@ L = tqr.lib()
 m = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 n = int(sys.argv[2]) if len(sys.argv) > 2 else m
 b = int(sys.argv[3]) if len(sys.argv) > 3 else 256
-A = torch.empty((n, m), dtype=torch.float64, device="cuda")
-tau = torch.zeros((min(m, n) // b, m), dtype=torch.float64, device="cuda")
-p = tqr.TiledQR(m, n, b, torch.float64)
+dt = torch.float32 if os.environ.get("TQR_FST_DTYPE") == "f32" else torch.float64
+A = torch.empty((n, m), dtype=dt, device="cuda")
+tau = torch.zeros((min(m, n) // b, m), dtype=dt, device="cuda")
+p = tqr.TiledQR(m, n, b, dt)
 for rep in range(2):
     tqr.fill_randzo(A, m, n, 5)
     torch.cuda.synchronize()
