@@ -268,7 +268,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
         if (ok && !dma_next) ok = ready(i, 0);
       }
       FST(j == k + 1 ? 18 : 19);
-      if (!sync_point<false>(ok, sflag, par)) return;
+      if (!sync_point<false, true>(ok, sflag, par)) return;
     }
     FST(7);
     float* Xt = ts ? A + (size_t)j * B * ldm + (size_t)i * B : At;
@@ -317,7 +317,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
             }
           }
           FST(j == k + 1 ? 20 : 0);
-          if (!sync_point<true>(ok, sflag, par)) return false;
+          if (!sync_point<true, true>(ok, sflag, par)) return false;
         }
         if (g == 0 && pending) {
           publish_after_drain(pending, 1);
@@ -408,7 +408,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
     pending = tc(i);
     FST(4);
   }
-  sync_point<true>(true, sflag, par);
+  sync_point<true, true>(true, sflag, par);
   if (pending) publish_after_drain(pending, 1);
   publish_after_drain(&acg[NG - 1], 1);
   FST(4);

@@ -63,8 +63,26 @@ extern __device__ unsigned long long g_ttl[];  // per task: start, end (s_memrea
       l_[0] = n_;                                                                         \
     }                                                                                     \
   } while (0)
+// per-wave sync accounting (all 8 waves, lane 0): [wave][0] own-memory drain, [wave][1] barrier
+// wait, summed over the chain sync points (LDS tail ints 128.., written to g_wst at exit)
+extern __device__ unsigned long long g_wst[];
+#define WST_T0() const unsigned long long wst0_ = __builtin_amdgcn_s_memrealtime()
+#define WST_ACC(slot, tref)                                                                        \
+  do {                                                                                             \
+    const unsigned long long n_ = __builtin_amdgcn_s_memrealtime();                                \
+    if ((threadIdx.x & 63) == 0) {                                                                 \
+      __attribute__((address_space(3))) unsigned long long* w_ =                                   \
+          (__attribute__((address_space(3))) unsigned long long*)(sflag + 127) + 2 * (threadIdx.x >> 6); \
+      w_[slot] += n_ - (tref);                                                                     \
+    }                                                                                              \
+  } while (0)
+#define WST_MID() const unsigned long long wst1_ = __builtin_amdgcn_s_memrealtime(); WST_ACC(0, wst0_)
+#define WST_END() WST_ACC(1, wst1_)
 #else
 #define FST(c) do {} while (0)
+#define WST_T0() do {} while (0)
+#define WST_MID() do {} while (0)
+#define WST_END() do {} while (0)
 #endif
 // 512 threads = 8 waves = two waves per SIMD: a chain task updates a 128-column strip, so each
 // LDS-DMA'd V/T image serves twice the flops of the 4-wave / 64-column form, and each SIMD's
@@ -158,11 +176,20 @@ __device__ __noinline__ bool spin_ge(int* p, int target, int* err, bool sys = fa
 // bytes with sc1 loads — no release / acquire fences (each ~1.7 us at one workgroup per CU).
 // The chain's LDS-DMA of V/T images reads write-once data (see PanelView) and needs neither.
 
+// The LDS tail words (task word, verdicts, flags, Rc view) reach the task functions as generic
+// pointers; accessed through them (volatile ones are never rewritten to LDS) they become flat
+// operations, which count in vmcnt as well: the wait for a flat verdict read after a sync point
+// was an s_waitcnt vmcnt(0) — a full drain of the wave's memory operations behind every partial
+// drain. Every access to those words goes through an LDS-typed pointer (ds_read/ds_write).
+typedef __attribute__((address_space(3))) int lds_int_t;
+__device__ __forceinline__ lds_int_t* lds_int(int* p) { return (lds_int_t*)p; }
+__device__ __forceinline__ int lds_ld_volatile(int* p) { return *(volatile lds_int_t*)lds_int(p); }
+
 // all threads: thread 0's verdict (after its polls)
 __device__ __forceinline__ bool wg_verdict(bool ok0, int* sflag) {
-  if (threadIdx.x == 0) *sflag = ok0 ? 1 : 0;
+  if (threadIdx.x == 0) *lds_int(sflag) = ok0 ? 1 : 0;
   __syncthreads();
-  const bool ok = *sflag != 0;
+  const bool ok = lds_ld_volatile(sflag) != 0;
   __syncthreads();
   return ok;
 }
@@ -248,16 +275,23 @@ struct DmaJob {
 // to). Optionally drain this wave's vector-memory operations (its LDS-DMA landed, loads and
 // stores complete), one raw barrier (no implicit vmcnt(0)), then every wave reads the verdict
 // from a parity-alternating LDS slot (a slot is rewritten only after the next barrier).
-template <bool DRAIN>
+// FLAT: the verdict read as a generic (flat) load — its wait is vmcnt(0), i.e. a full drain, which
+// only the fp32 chain still uses (its register allocation spills in the phase loops otherwise;
+// every sync point there drains fully anyway).
+template <bool DRAIN, bool FLAT = false>
 __device__ __forceinline__ bool sync_point(bool ok0, int* sflag, int& par) {
   int* slot = sflag + 40 + par;  // LDS tail (ints from the task word): [task][flag][..][verdicts 41,42][..][Rc view 49..][..][FST sums 64..]
   par ^= 1;
-  if (threadIdx.x == 0) *slot = ok0 ? 1 : 0;
+  if (threadIdx.x == 0) *lds_int(slot) = ok0 ? 1 : 0;
+  WST_T0();
   if (DRAIN) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  WST_MID();
   __builtin_amdgcn_s_barrier();
+  WST_END();
   asm volatile("" ::: "memory");
-  return *(volatile int*)slot != 0;
+  if constexpr (FLAT) return *(volatile int*)slot != 0;
+  return lds_ld_volatile(slot) != 0;
 }
 // A group's sync point inside a segment: only the LDS-DMA of this group (issued in the previous
 // group's phase 1) and everything older must have landed; the N youngest operations — the
@@ -268,12 +302,15 @@ template <int N>
 __device__ __forceinline__ bool sync_point_cnt(bool ok0, int* sflag, int& par) {
   int* slot = sflag + 40 + par;
   par ^= 1;
-  if (threadIdx.x == 0) *slot = ok0 ? 1 : 0;
+  if (threadIdx.x == 0) *lds_int(slot) = ok0 ? 1 : 0;
   static_assert(N >= 0 && N < 64, "vmcnt range");
+  WST_T0();
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+  WST_MID();
   __builtin_amdgcn_s_barrier();
+  WST_END();
   asm volatile("" ::: "memory");
-  return *(volatile int*)slot != 0;
+  return lds_ld_volatile(slot) != 0;
 }
 // The first group's sync point of an element: everything older than the element's own strip and
 // head loads (the previous element's stores, this group's LDS-DMA) must be complete, the NX
@@ -284,13 +321,16 @@ template <int NX>
 __device__ __forceinline__ bool sync_point_first(bool ok0, int* sflag, int& par, bool loaded) {
   int* slot = sflag + 40 + par;
   par ^= 1;
-  if (threadIdx.x == 0) *slot = ok0 ? 1 : 0;
+  if (threadIdx.x == 0) *lds_int(slot) = ok0 ? 1 : 0;
   static_assert(NX >= 0 && NX < 64, "vmcnt range");
+  WST_T0();
   if (loaded) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NX) : "memory");
   else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  WST_MID();
   __builtin_amdgcn_s_barrier();
+  WST_END();
   asm volatile("" ::: "memory");
-  return *(volatile int*)slot != 0;
+  return lds_ld_volatile(slot) != 0;
 }
 // thread 0, after a draining sync point (every wave's sc1 stores complete): bump a counter
 __device__ __forceinline__ void publish_after_drain(int* p, int delta) {
@@ -307,11 +347,11 @@ __device__ __forceinline__ void publish_after_drain(int* p, int delta) {
 // ensure() normally finds fresh values without an exposed round trip.
 template <int NG>
 struct PanelView {
-  int* rv;
+  lds_int_t* rv;
   int pf[NG];
   bool pf_valid;
   __device__ __forceinline__ void init(int* lds_words) {
-    rv = lds_words;
+    rv = lds_int(lds_words);
     pf_valid = false;
     if (threadIdx.x == 0)
       for (int g = 0; g < NG; ++g) rv[g] = 0;
@@ -344,28 +384,28 @@ struct PanelView {
 
 // Two consecutive elements (a row pair of a column) as one sc1 buffer access: 16 B for fp64,
 // 8 B for fp32 storage.
-template <typename S>
+template <typename S, int AUX = 16>
 __device__ __forceinline__ void ld_pair(__amdgpu_buffer_rsrc_t rs, unsigned off, double& a, double& b) {
   if constexpr (sizeof(S) == 8) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUX);
     a = __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
     b = __longlong_as_double((long long)(((unsigned long long)v[3] << 32) | v[2]));
   } else {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 16);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, AUX);
     a = (double)__uint_as_float(v[0]);
     b = (double)__uint_as_float(v[1]);
   }
 }
-template <typename S>
+template <typename S, int AUX = 16>
 __device__ __forceinline__ void st_pair(__amdgpu_buffer_rsrc_t rs, unsigned off, double a, double b) {
   if constexpr (sizeof(S) == 8) {
     const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
     const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
     __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)ua, (unsigned)(ua >> 32), (unsigned)ub, (unsigned)(ub >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, AUX);
   } else {
     __attribute__((ext_vector_type(2))) unsigned v = {__float_as_uint((float)a), __float_as_uint((float)b)};
-    __builtin_amdgcn_raw_buffer_store_b64(v, rs, off, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b64(v, rs, off, 0, AUX);
   }
 }
 
@@ -569,6 +609,19 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
 }
 
 // ---- chain tasks ---------------------------------------------------------------------------
+// MFMA-issue fairness between the two waves of a SIMD (waves w and w + 4): the issue arbiter
+// favours the older wave, which then finished its group's MFMAs early and sat at the group's
+// barrier while its partner ran alone, every dependency and LDS bubble of a single wave exposed
+// (stamps: waves 1-3 waited 44 ms per workgroup at the barriers, waves 5-7 11 ms). Phase 1
+// favours the upper waves, phase 2 the lower ones, so the pair ends its group together.
+__device__ __forceinline__ void phase_prio(bool phase2) {
+#ifndef TQR_NO_PRIO
+  const bool upper = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4;
+  if (upper != phase2) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
 // Element hand-over inside the last group's phase 2 (apply_x post hook): once row pair h-1 of the
 // strip is final, it is stored (write-through) and the same registers start loading pair h-1 of
 // the next element's strip — the strip's 512 B per lane out and in ride the MFMA stream instead
@@ -579,8 +632,8 @@ struct XPipe {
   unsigned base;
   __device__ __forceinline__ void xfer(int h, double (&X)[Geo<B>::NKS]) const {
     const unsigned so = base + 8 * h * sizeof(S);
-    st_pair<S>(out, so, X[2 * h], X[2 * h + 1]);
-    ld_pair<S>(in, so, X[2 * h], X[2 * h + 1]);
+    st_pair<S, TQR_STRIP_ST_AUX>(out, so, X[2 * h], X[2 * h + 1]);
+    ld_pair<S, TQR_STRIP_LD_AUX>(in, so, X[2 * h], X[2 * h + 1]);
   }
   __device__ __forceinline__ void at(int h, double (&X)[Geo<B>::NKS]) const {
     if (h >= 1) xfer(h - 1, X);  // pair h-1 retired one k-step pair ago
@@ -720,6 +773,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
                      : full ? sync_point<true>(ok, sflag, par) : sync_point_cnt<NH>(ok, sflag, par)))
           return false;
       }
+      // (flat read of an LDS word: read here, where little is in flight, as its wait is vmcnt(0))
+      bool pipe = false;
+      if (g + 1 == NG) pipe = *(volatile int*)(sflag + 44) != 0;  // (written before this sync point)
       // the previous element's strip stores are drained: at group 0 (stored before this
       // element's loads) or, after a streamed hand-over (stores interleaved with the loads), at 1
       if (g == (xin ? 1 : 0) && pending) {
@@ -754,6 +810,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
 #ifdef TQR_DIAG_NODMA  // what-if: no staging at all
       if (active) apply_zw<B, true, NoHook, FLOW_PF, true>(Vs, Ts, X, H, W, 0);
 #else
+      phase_prio(false);
       if (active) apply_zw<B, true, DmaJob<B>, FLOW_PF, true>(Vs, Ts, X, H, W, 0, d);
       else
         for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
@@ -771,8 +828,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       }
 #endif
       FST(14);
-      bool pipe = false;
-      if (g + 1 == NG) pipe = *(volatile int*)(sflag + 44) != 0;  // (written before this sync point)
+      phase_prio(true);
       if (active) {
         if (pipe) {
           S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
@@ -830,6 +886,8 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
     unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 64);
     l_[0] = __builtin_amdgcn_s_memrealtime();
     for (int c = 0; c < FST_N; ++c) l_[1 + c] = 0;
+    unsigned long long* w_ = reinterpret_cast<unsigned long long*>(s_task + 128);
+    for (int c = 0; c < 16; ++c) w_[c] = 0;
   }
   int* sflag = s_flag;
 #endif
@@ -873,6 +931,8 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
   if (threadIdx.x == 0) {
     unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 64);
     for (int c = 0; c < FST_N; ++c) g_fst[blockIdx.x * FST_N + c] = l_[1 + c];
+    const unsigned long long* w_ = reinterpret_cast<const unsigned long long*>(s_task + 128);
+    for (int c = 0; c < 16; ++c) g_wst[blockIdx.x * 16 + c] = w_[c];
   }
 #endif
 }

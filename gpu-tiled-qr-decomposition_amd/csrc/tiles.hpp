@@ -26,6 +26,14 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// cache policy of the strip traffic (tile strips streamed once per step): aux bits of the buffer
+// loads / stores (16 = sc1 write-through / L1 bypass, | 2 = nt streaming)
+#ifndef TQR_STRIP_LD_AUX
+#define TQR_STRIP_LD_AUX 16
+#endif
+#ifndef TQR_STRIP_ST_AUX
+#define TQR_STRIP_ST_AUX 16
+#endif
 namespace tqr {
 
 #ifdef TQR_STAMPS
@@ -145,6 +153,17 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 // hook.step(m) is called once per two k-steps of phase 1 (m = 0, 1, ...) inside the MFMA
 // stream, then for the remaining m < Hook::STEPS after the loop: the chain engine issues the
 // next group's LDS-DMA there (flow.hpp), so its issue cost hides under the MFMAs.
+// LDS operand addressing: the byte address of p as an opaque 32-bit value (the optimizer cannot
+// re-derive it per use), and a 16-B read at such an address
+typedef double d2v_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) const d2v_t lds_cd2_t;
+__device__ __forceinline__ unsigned lds_base(const double* p) {
+  unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
+  asm volatile("" : "+v"(a));
+  return a;
+}
+__device__ __forceinline__ d2v_t lds_rd2(unsigned a) { return *(lds_cd2_t*)(size_t)a; }
+
 struct NoHook {
   __device__ __forceinline__ void step(int) const {}
   __device__ __forceinline__ void mid() const {}  // between Z and W (activity stamps)
@@ -167,11 +186,14 @@ __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const do
   // Z += V^T X   (A operand: V[4ks+x][4ri+y]); software-pipelined: the LDS reads of k-step
   // ks+1 are issued ahead of the MFMAs of ks (one wave per SIMD cannot hide LDS latency
   // otherwise; tools/ubench/apply_bench.hip: 73 % -> 83 % of peak)
+  // one opaque lane base + a per-k-step constant (immediate offsets): left to the optimizer the
+  // row index was re-formed per k-step as (4ks | x), some of those products were kept in VGPRs,
+  // spilled, and their reloads inside the MFMA stream waited (vmcnt(0)) for the LDS-DMA
+  const unsigned vz = lds_base(Vs + x * VP + y * NRI);
   auto ldz = [&](double (&a)[NRI], int ks) {
-    const double2* vr = reinterpret_cast<const double2*>(Vs + (4 * ks + x) * VP + y * NRI);
 #pragma unroll
     for (int h = 0; h < NRI / 2; ++h) {
-      const double2 t = vr[h];
+      const d2v_t t = lds_rd2(vz + (unsigned)((4 * ks * VP + 2 * h) * sizeof(double)));
       a[2 * h] = t.x;
       a[2 * h + 1] = t.y;
     }
@@ -254,11 +276,11 @@ __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&
   constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP;
   const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
   // X += V W   (A operand: V[4ks+y][4wi+x]); two k-steps per region, next pair's reads ahead.
+  const unsigned vx = lds_base(Vs + y * VP + x * NRI);  // (see apply_zw)
   auto ldx = [&](double (&a)[NRI], int ks) {
-    const double2* vr = reinterpret_cast<const double2*>(Vs + (4 * ks + y) * VP + x * NRI);
 #pragma unroll
     for (int h = 0; h < NRI / 2; ++h) {
-      const double2 t = vr[h];
+      const d2v_t t = lds_rd2(vx + (unsigned)((4 * ks * VP + 2 * h) * sizeof(double)));
       a[2 * h] = t.x;
       a[2 * h + 1] = t.y;
     }
@@ -370,11 +392,11 @@ __device__ __forceinline__ void load_strip_pair(double (&X)[Geo<B>::NKS], S* til
     }
     const int so = 8 * h * sizeof(S);
     if constexpr (sizeof(S) == 8) {
-      auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, base, so, 16);
+      auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, base, so, TQR_STRIP_LD_AUX);
       X[2 * h] = __longlong_as_double(((long long)v[1] << 32) | v[0]);
       X[2 * h + 1] = __longlong_as_double(((long long)v[3] << 32) | v[2]);
     } else {
-      auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, base, so, 16);
+      auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, base, so, TQR_STRIP_LD_AUX);
       X[2 * h] = (double)__uint_as_float(v[0]);
       X[2 * h + 1] = (double)__uint_as_float(v[1]);
     }
@@ -394,10 +416,10 @@ __device__ __forceinline__ void store_strip_pair(const double (&X)[Geo<B>::NKS],
       const unsigned long long a = (unsigned long long)__double_as_longlong(X[2 * h]);
       const unsigned long long b = (unsigned long long)__double_as_longlong(X[2 * h + 1]);
       __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
-      __builtin_amdgcn_raw_buffer_store_b128(v, rs, base, so, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, base, so, TQR_STRIP_ST_AUX);
     } else {
       __attribute__((ext_vector_type(2))) unsigned v = {__float_as_uint((float)X[2 * h]), __float_as_uint((float)X[2 * h + 1])};
-      __builtin_amdgcn_raw_buffer_store_b64(v, rs, base, so, 16);
+      __builtin_amdgcn_raw_buffer_store_b64(v, rs, base, so, TQR_STRIP_ST_AUX);
     }
   }
 }

@@ -38,3 +38,10 @@ for c, nm in ((5, "panel_factor"), (11, "build_t"), (12, "trailing"), (10, "pane
     print(f"  per panel group ({npanel * ng} groups): {nm:14s} {tot[c] / (npanel * ng) / 100:7.2f} us")
 for c in range(NC):
     print(f"  {names[c]:24s} {tot[c] / nb / 1e5:8.2f} ms/WG  {100.0 * tot[c] / allt:5.1f}%")
+ws = (ctypes.c_ulonglong * (16 * nb))()
+if hasattr(L, "tqr_debug_flow_wave_stamps") and L.tqr_debug_flow_wave_stamps(ws, nb) == 0:
+    print("  per-wave chain sync sums (ms/WG): own-memory drain | barrier wait")
+    for w in range(8):
+        dr = sum(ws[b * 16 + 2 * w] for b in range(nb)) / nb / 1e5
+        br = sum(ws[b * 16 + 2 * w + 1] for b in range(nb)) / nb / 1e5
+        print(f"    wave {w}: {dr:7.2f} | {br:7.2f}")

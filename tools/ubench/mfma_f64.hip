@@ -129,6 +129,12 @@ int main() {
     RUN("mfma_f64_16x16x4 x4acc", (k_mfma<4><<<blocks, 256>>>(out, clk, iters, 1e-3)), (double)blocks * 4 * iters * 4 * 2048.0);
     RUN("mfma_f64_16x16x4 x8acc", (k_mfma<8><<<blocks, 256>>>(out, clk, iters / 2, 1e-3)), (double)blocks * 4 * (iters / 2) * 8 * 2048.0);
     RUN("mfma_f64_4x4x4_4b x8acc", (k_mfma4<8><<<blocks, 256>>>(out, clk, iters, 1e-3)), (double)blocks * 4 * iters * 8 * 512.0);
+    // dependent-accumulator latency: fewer independent chains than the latency / issue ratio
+    // leave the pipe idle (one wave per SIMD shows it directly)
+    RUN("mfma_f64_4x4x4_4b x1acc", (k_mfma4<1><<<blocks, 256>>>(out, clk, iters, 1e-3)), (double)blocks * 4 * iters * 1 * 512.0);
+    RUN("mfma_f64_4x4x4_4b x2acc", (k_mfma4<2><<<blocks, 256>>>(out, clk, iters, 1e-3)), (double)blocks * 4 * iters * 2 * 512.0);
+    RUN("mfma_f64_4x4x4_4b x3acc", (k_mfma4<3><<<blocks, 256>>>(out, clk, iters, 1e-3)), (double)blocks * 4 * iters * 3 * 512.0);
+    RUN("mfma_f64_4x4x4_4b x4acc", (k_mfma4<4><<<blocks, 256>>>(out, clk, iters, 1e-3)), (double)blocks * 4 * iters * 4 * 512.0);
     RUN("mfma_f32_16x16x4 x8acc", (k_mfma32<0, 8><<<blocks, 256>>>((float*)out, clk, iters / 2, 1e-3f)), (double)blocks * 4 * (iters / 2) * 8 * 2048.0);
     RUN("mfma_f32_32x32x2 x4acc", (k_mfma32<1, 4><<<blocks, 256>>>((float*)out, clk, iters / 2, 1e-3f)), (double)blocks * 4 * (iters / 2) * 4 * 4096.0);
     RUN("mfma_f32_4x4x1_16b x8acc", (k_mfma32<2, 8><<<blocks, 256>>>((float*)out, clk, iters, 1e-3f)), (double)blocks * 4 * iters * 8 * 512.0);
