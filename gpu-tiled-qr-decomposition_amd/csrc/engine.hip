@@ -63,7 +63,7 @@ __device__ unsigned long long g_pstamps[8];
 #ifdef TQR_FLOW_STAMPS
 __device__ unsigned long long g_fst[4096 * 24];  // >= FST_N categories per workgroup
 __device__ unsigned long long g_ttl[3 << 18];     // task timeline (first 2^18 tasks)
-__device__ unsigned long long g_wst[4096 * 16];   // per-wave sync drain / barrier sums
+__device__ unsigned long long g_wst[4096 * 64];   // per-wave activity sums (flow.hpp WSL slots x 8 waves)
 #endif
 }  // namespace tqr
 #include "flow.hpp"
@@ -317,7 +317,7 @@ static size_t lds_flow(int b, int dtype) {
   case BB: d = dtype == TQR_F64 ? flow_lds_doubles<BB, double>() : flow_lds_doubles<BB, float>(); break;
   switch (b) { TQR_L(16) TQR_L(32) TQR_L(64) TQR_L(128) TQR_L(256) }
 #undef TQR_L
-  return (size_t)d * sizeof(double) + 1024;  // + task index, sync-point verdicts, Rc view, FST sums, wave sums
+  return (size_t)d * sizeof(double) + 1536;  // + task index, sync-point verdicts, Rc view, FST sums, wave sums
 }
 static ffn resolve_flow(int b, int dtype) {
   ffn f = nullptr;
@@ -1538,10 +1538,10 @@ extern "C" int tqr_debug_flow_stamps(unsigned long long* out, int nblocks) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fst), sizeof(unsigned long long) * FST_N * nblocks) != hipSuccess) return TQR_EHIP;
   return TQR_OK;
 }
-// per-wave sync sums of the last k_flow launch: [workgroup][wave][own drain, barrier wait]
+// per-wave activity sums of the last k_flow launch: [workgroup][wave][WSL slots, flow.hpp]
 extern "C" int tqr_debug_flow_wave_stamps(unsigned long long* out, int nblocks) {
   if (nblocks > 4096) return TQR_EINVAL;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wst), sizeof(unsigned long long) * 16 * nblocks) != hipSuccess) return TQR_EHIP;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wst), sizeof(unsigned long long) * 8 * WSL * nblocks) != hipSuccess) return TQR_EHIP;
   return TQR_OK;
 }
 // task timeline of the last k_flow launch: (start, end, workgroup) per task index, and the task list

@@ -51,6 +51,7 @@ constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel memb
 // includes the element's strip loads, which the real kernel overlaps with phase 1), 23 forward
 // tasks (multi-GPU: panel images copied to the peers, including their waits for the panel).
 constexpr int FST_N = 24;
+constexpr int WSL = 8;  // per-wave stamp slots
 #ifdef TQR_FLOW_STAMPS
 extern __device__ unsigned long long g_fst[];
 extern __device__ unsigned long long g_ttl[];  // per task: start, end (s_memrealtime), workgroup
@@ -63,8 +64,10 @@ extern __device__ unsigned long long g_ttl[];  // per task: start, end (s_memrea
       l_[0] = n_;                                                                         \
     }                                                                                     \
   } while (0)
-// per-wave sync accounting (all 8 waves, lane 0): [wave][0] own-memory drain, [wave][1] barrier
-// wait, summed over the chain sync points (LDS tail ints 128.., written to g_wst at exit)
+// per-wave accounting (all 8 waves, lane 0; LDS tail ints 128.., written to g_wst at exit), WSL
+// slots per wave: 0 own-memory drain and 1 barrier wait at the chain sync points; the fp64 chain's
+// group loop (WMARK): 2 before the sync (polls), 3 after it (publish, setup), 4 phase 1 (Z, W, H),
+// 5 head I/O, 6 phase 2, 7 after phase 2 (next-head hand-over, loop)
 extern __device__ unsigned long long g_wst[];
 #define WST_T0() const unsigned long long wst0_ = __builtin_amdgcn_s_memrealtime()
 #define WST_ACC(slot, tref)                                                                        \
@@ -72,15 +75,23 @@ extern __device__ unsigned long long g_wst[];
     const unsigned long long n_ = __builtin_amdgcn_s_memrealtime();                                \
     if ((threadIdx.x & 63) == 0) {                                                                 \
       __attribute__((address_space(3))) unsigned long long* w_ =                                   \
-          (__attribute__((address_space(3))) unsigned long long*)(sflag + 127) + 2 * (threadIdx.x >> 6); \
+          (__attribute__((address_space(3))) unsigned long long*)(sflag + 127) + WSL * (threadIdx.x >> 6); \
       w_[slot] += n_ - (tref);                                                                     \
     }                                                                                              \
   } while (0)
 #define WST_MID() const unsigned long long wst1_ = __builtin_amdgcn_s_memrealtime(); WST_ACC(0, wst0_)
 #define WST_END() WST_ACC(1, wst1_)
+#define WMARK_INIT() unsigned long long wt_ = __builtin_amdgcn_s_memrealtime()
+#define WMARK(slot)                     \
+  do {                                  \
+    WST_ACC(slot, wt_);                 \
+    wt_ = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
 #define FST(c) do {} while (0)
 #define WST_T0() do {} while (0)
+#define WMARK_INIT() do {} while (0)
+#define WMARK(slot) do {} while (0)
 #define WST_MID() do {} while (0)
 #define WST_END() do {} while (0)
 #endif
@@ -737,7 +748,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     // the group loop as a lambda with a single exit (an early return out of the loop itself made
     // the register allocator spill ~1 KiB around the poll calls)
     auto groups = [&]() -> bool {
+    WMARK_INIT();
     for (int g = 0; g < NG; ++g) {
+      WMARK(7);
       {
         bool ok = true;
 #ifdef TQR_FLOW_STAMPS
@@ -768,10 +781,14 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         // full drain where a publish follows: the segment's last element (head rows, Ac) and the
         // first group after a streamed hand-over (the previous element's strip stores, Tc)
         const bool full = !has_next || (xin && g == 1);
+        WMARK(2);
         constexpr int NH = FLOW_PF ? 2 * G::NRI : G::NRI;  // head stores + next head loads
         if (!(g == 0 ? sync_point_first<NX>(ok, sflag, par, active)
                      : full ? sync_point<true>(ok, sflag, par) : sync_point_cnt<NH>(ok, sflag, par)))
           return false;
+#ifdef TQR_FLOW_STAMPS
+        wt_ = __builtin_amdgcn_s_memrealtime();  // (the sync point's own time is in slots 0, 1)
+#endif
       }
       // (flat read of an LDS word: read here, where little is in flight, as its wait is vmcnt(0))
       bool pipe = false;
@@ -811,11 +828,13 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       if (active) apply_zw<B, true, NoHook, FLOW_PF, true>(Vs, Ts, X, H, W, 0);
 #else
       phase_prio(false);
+      WMARK(3);
       if (active) apply_zw<B, true, DmaJob<B>, FLOW_PF, true>(Vs, Ts, X, H, W, 0, d);
       else
         for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
 #endif
       FST(15);
+      WMARK(4);
 #ifndef TQR_DIAG_NOHEAD
       if (active) {
         // head rows stay with this workgroup inside the segment (plain write-back stores); the
@@ -828,6 +847,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       }
 #endif
       FST(14);
+      WMARK(5);
       phase_prio(true);
       if (active) {
         if (pipe) {
@@ -841,6 +861,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       }
       if (g + 1 == NG) xin = pipe;
       FST(13);
+      WMARK(6);
       if (FLOW_PF) {
 #pragma unroll
         for (int r = 0; r < G::NRI; ++r) H[r] = Hn[r];
@@ -862,6 +883,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   publish_after_drain(&acg[NG - 1], 1);
   FST(4);
 }
+
 
 }  // namespace tqr
 #include "chain32.hpp"
@@ -887,7 +909,7 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
     l_[0] = __builtin_amdgcn_s_memrealtime();
     for (int c = 0; c < FST_N; ++c) l_[1 + c] = 0;
     unsigned long long* w_ = reinterpret_cast<unsigned long long*>(s_task + 128);
-    for (int c = 0; c < 16; ++c) w_[c] = 0;
+    for (int c = 0; c < 8 * WSL; ++c) w_[c] = 0;
   }
   int* sflag = s_flag;
 #endif
@@ -932,7 +954,7 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
     unsigned long long* l_ = reinterpret_cast<unsigned long long*>(s_task + 64);
     for (int c = 0; c < FST_N; ++c) g_fst[blockIdx.x * FST_N + c] = l_[1 + c];
     const unsigned long long* w_ = reinterpret_cast<const unsigned long long*>(s_task + 128);
-    for (int c = 0; c < 16; ++c) g_wst[blockIdx.x * 16 + c] = w_[c];
+    for (int c = 0; c < 8 * WSL; ++c) g_wst[blockIdx.x * 8 * WSL + c] = w_[c];
   }
 #endif
 }

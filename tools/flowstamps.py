@@ -38,10 +38,11 @@ for c, nm in ((5, "panel_factor"), (11, "build_t"), (12, "trailing"), (10, "pane
     print(f"  per panel group ({npanel * ng} groups): {nm:14s} {tot[c] / (npanel * ng) / 100:7.2f} us")
 for c in range(NC):
     print(f"  {names[c]:24s} {tot[c] / nb / 1e5:8.2f} ms/WG  {100.0 * tot[c] / allt:5.1f}%")
-ws = (ctypes.c_ulonglong * (16 * nb))()
+WSL = 8
+ws = (ctypes.c_ulonglong * (8 * WSL * nb))()
 if hasattr(L, "tqr_debug_flow_wave_stamps") and L.tqr_debug_flow_wave_stamps(ws, nb) == 0:
-    print("  per-wave chain sync sums (ms/WG): own-memory drain | barrier wait")
+    wn = ["drain", "barrier", "pre-sync", "post-sync", "phase1", "head I/O", "phase2", "tail"]
+    print("  per-wave sums (ms/WG): " + " | ".join(f"{n:>9s}" for n in wn))
     for w in range(8):
-        dr = sum(ws[b * 16 + 2 * w] for b in range(nb)) / nb / 1e5
-        br = sum(ws[b * 16 + 2 * w + 1] for b in range(nb)) / nb / 1e5
-        print(f"    wave {w}: {dr:7.2f} | {br:7.2f}")
+        v = [sum(ws[b * 8 * WSL + WSL * w + c] for b in range(nb)) / nb / 1e5 for c in range(WSL)]
+        print(f"    wave {w}:            " + " | ".join(f"{x:9.2f}" for x in v) + f" | sum {sum(v):7.2f}")
