@@ -854,9 +854,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
           S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
           const XPipe<B, S> xp{uniform_rsrc(Xt + (size_t)col * ldm), uniform_rsrc(Xn + (size_t)col * ldm),
                                (unsigned)((((size_t)(t & 15)) * ldm + 2 * ((t & 63) >> 4)) * sizeof(S))};
-          apply_x<B, true, FLOW_PF, NoHook, XPipe<B, S>>(Vs, X, W, 0, NoHook(), xp);
+          apply_x4<B, XPipe<B, S>>(Vs, X, W, xp);
         } else {
-          apply_x<B, true, FLOW_PF>(Vs, X, W, 0);
+          apply_x4<B>(Vs, X, W);
         }
       }
       if (g + 1 == NG) xin = pipe;

@@ -321,6 +321,55 @@ __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&
   for (int m = NKS / 2; m < Hook::STEPS; ++m) hook.step(m);
 }
 
+// Chain form of phase 2 (TS-type, all k-steps): X += V W over blocks of 4 k-steps, the group's
+// reflectors in two halves, so 4 independent accumulation chains are interleaved (the 4x4x4 f64
+// form's dependent latency is ~40 cycles, 2.5 instructions: with apply_x's 2 chains a wave alone
+// on its SIMD issues at 64 %, with 3-4 at 93-96 %, profiles/r02/ubench_mfma_f64_latency.txt —
+// the end of every group, when one wave of a pair has finished, runs on one wave). Operand
+// registers as apply_x: 4 k-steps x NRI/2 values, the next half read ahead.
+template <int B, typename Post = NoPost>
+__device__ __forceinline__ void apply_x4(const double* __restrict__ Vs, double (&X)[Geo<B>::NKS],
+                                         const double (&W)[Geo<B>::NRI], const Post& post = Post()) {
+  using g = Geo<B>;
+  constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP, NH = NRI / 2;
+  static_assert(NKS % 4 == 0 && NH % 2 == 0, "apply_x4 blocks");
+  const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
+  const unsigned vx = lds_base(Vs + y * VP + x * NRI);  // (see apply_zw)
+  auto ldh = [&](double (&a)[4][NH], int kb, int half) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < NH / 2; ++q) {
+        const d2v_t t = lds_rd2(vx + (unsigned)((4 * (kb + u) * VP + half * NH + 2 * q) * sizeof(double)));
+        a[u][2 * q] = t.x;
+        a[u][2 * q + 1] = t.y;
+      }
+  };
+  double oc[4][NH], on[4][NH];
+  ldh(oc, 0, 0);
+#pragma unroll
+  for (int kb = 0; kb < NKS; kb += 4) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      __builtin_amdgcn_sched_barrier(0);  // (see apply_zw)
+      asm volatile("" ::: "memory");
+      if (half == 0) ldh(on, kb, 1);
+      else if (kb + 4 < NKS) ldh(on, kb + 4, 0);
+#pragma unroll
+      for (int q = 0; q < NH; ++q)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) X[kb + u] = mfma4(oc[u][q], W[half * NH + q], X[kb + u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < NH; ++q) oc[u][q] = on[u][q];
+    }
+    post.at(kb / 2, X);
+    post.at(kb / 2 + 1, X);
+  }
+  post.fin(X);
+}
+
 template <int B, bool HEAD, bool PF = true, bool TPACK = false>
 __device__ __forceinline__ void apply_group(const double* __restrict__ Vs, const double* __restrict__ Ts,
                                             double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI], int ks0) {
