@@ -20,7 +20,7 @@
 //     Hd is rotated by NMI tiles per group, so the current group's rows are always Hd[0..NMI);
 //   * per group: Z = Hd[0..NMI) + V^T X (NMT x 4 x NMI MFMAs), W = -T^T Z (4 NPR), Hd += W,
 //     X += V W (NMT x 4 x NMI); the UNMQR element runs Z = V^T Hd, Hd += V W (explicit GE V).
-// The images (VA, VB, TP; tiles.hpp Geo32) are written by the panel task from its fp64 LDS block
+// The images (VR, TP; tiles.hpp Geo32) are written by the panel task from its fp64 LDS block
 // (the panel itself factorises in fp64 and stores fp32 V, R, tau) and LDS-DMA'd like the fp64 ones.
 #pragma once
 
@@ -55,22 +55,15 @@ __device__ __noinline__ void write_images32(const double* Vs, const double* Ts, 
   using G32 = Geo32<B>;
   constexpr int NMI = G32::NMI, VP = G::VP, TP = G::TP;
   auto V = [&](int R, int c) { return (float)Vs[vimg_inv(R) * VP + G::pc(c)]; };
-  for (int idx = threadIdx.x; idx < G32::VA / 4; idx += blockDim.x) {  // VA chunks
-    const int lane = idx & 63, mc = idx >> 6, ch = mc % NMI, mt = mc / NMI, x = lane >> 4, y = lane & 15;
+  for (int idx = threadIdx.x; idx < G32::VR / 4; idx += blockDim.x) {  // VR 16-B chunks
+    const int R = idx / (G32::IB / 4), slot = (idx % (G32::IB / 4)) ^ G32::vr_sw(R);
     f4v v;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int q = ch * 4 + e, r = q / NMI, mi = q % NMI;
-      v[e] = V(16 * mt + 4 * x + r, 16 * mi + sig16(y));
+      const int p = 4 * slot + e, x = p / (4 * NMI), wi = (p >> 2) % NMI, r = p & 3;
+      v[e] = V(R, 16 * wi + 4 * x + r);
     }
     st_f4(rv, 16u * idx, v);
-  }
-  for (int idx = threadIdx.x; idx < G32::VB / 4; idx += blockDim.x) {  // VB chunks
-    const int lane = idx & 63, mc = idx >> 6, wi = mc % NMI, mt = mc / NMI, x = lane >> 4, y = lane & 15;
-    f4v v;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = V(16 * mt + sig16(y), 16 * wi + 4 * x + r);
-    st_f4(rv, 16u * (G32::VA / 4 + idx), v);
   }
   for (int idx = threadIdx.x; idx < G32::TIMG * 2 / 4; idx += blockDim.x) {  // TP chunks (+ zero pad)
     const int lane = idx & 63, pr = idx >> 6, x = lane >> 4, y = lane & 15;
@@ -86,6 +79,17 @@ __device__ __noinline__ void write_images32(const double* Vs, const double* Ts, 
     st_f4(rt, 16u * idx, v);
   }
 }
+
+// V image reads (Geo32 VR): opaque 32-bit LDS byte address (per-lane bases, immediate offsets)
+typedef __attribute__((address_space(3))) const float lds_cf_t;
+typedef __attribute__((address_space(3))) const f4v lds_cf4_t;
+__device__ __forceinline__ unsigned lds_addr_f(const float* p) {
+  unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
+  asm volatile("" : "+v"(a));
+  return a;
+}
+__device__ __forceinline__ float lds_rdf(unsigned a) { return *(lds_cf_t*)(size_t)a; }
+__device__ __forceinline__ f4v lds_rdf4(unsigned a) { return *(lds_cf4_t*)(size_t)a; }
 
 // LDS operand reads: NMI float4 chunks of tile mt for this lane
 template <int N>
@@ -134,23 +138,52 @@ struct XPipe32 {
 // the strip is the head tile itself). Phase 1 carries the hook (next group's LDS-DMA), phase 2
 // the post hook (element hand-over).
 template <int B, bool TS, typename Hook, typename Post = NoPost32>
-__device__ __forceinline__ void apply32(const float* VA, const float* VB, const float* TPi, f4v (&X)[Geo32<B>::NMT],
+__device__ __forceinline__ void apply32(const float* VR, const float* TPi, f4v (&X)[Geo32<B>::NMT],
                                         f4v (&Hg)[Geo32<B>::NMT], const Hook& hook, const Post& post = Post()) {
   using G32 = Geo32<B>;
   constexpr int NMT = G32::NMT, NMI = G32::NMI;
-  const int lane = threadIdx.x & 63;
+  constexpr int IB = G32::IB;
+  constexpr bool SW = IB == 32;
+  const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 15, q = y >> 2, e = y & 3;
+  // per-lane byte bases of the two phases' reads (Geo32::vr_at, unrolled by hand): phase 1 reads
+  // V(16mt + 4x + r, 16mi + y) — slot NMI q + mi of row R, swizzled by vr_sw(R), whose bits
+  // from r only flip mi (r >= 2); phase 2 reads the 16-B slot NMI x + wi of row 16mt + y
+  const int sx = SW ? ((x & 1) | (((x >> 1) & 1) << 2)) : 0;
+  const int sy = SW ? ((((y >> 1) ^ (y >> 2)) & 1) | (((y >> 3) & 1) << 2)) : 0;
+  const unsigned vb = lds_addr_f(VR);
+  unsigned b1[NMI], b2[NMI];
+#pragma unroll
+  for (int m = 0; m < NMI; ++m) {
+    b1[m] = vb + 4u * (4 * x * IB + (((NMI * q + m) ^ sx) << 2) + e);
+    b2[m] = vb + 4u * (y * IB + (((NMI * x + m) ^ sy) << 2));
+  }
+  auto ld1 = [&](float (&a)[4 * NMI], int mt) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int mi = 0; mi < NMI; ++mi)
+        a[r * NMI + mi] = lds_rdf(b1[SW ? (mi ^ ((r >> 1) & 1)) : mi] + 4u * ((16 * mt + r) * IB));
+  };
+  auto ld2 = [&](float (&a)[4 * NMI], int mt) {
+#pragma unroll
+    for (int wi = 0; wi < NMI; ++wi) {
+      const f4v t = lds_rdf4(b2[wi] + 4u * (16 * mt * IB));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[4 * wi + r] = t[r];
+    }
+  };
   f4v Z[NMI];
 #pragma unroll
   for (int mi = 0; mi < NMI; ++mi) Z[mi] = TS ? Hg[mi] : f4v{0.f, 0.f, 0.f, 0.f};
   // phase 1: Z += V^T X, operands of tile mt+1 read under the MFMAs of tile mt
   float ac[4 * NMI], an[4 * NMI];
-  ld_chunks<NMI>(ac, VA, 0, lane);
+  ld1(ac, 0);
 #pragma unroll
   for (int mt = 0; mt < NMT; ++mt) {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     hook.step(mt);
-    if (mt + 1 < NMT) ld_chunks<NMI>(an, VA, mt + 1, lane);
+    if (mt + 1 < NMT) ld1(an, mt + 1);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -179,19 +212,19 @@ __device__ __forceinline__ void apply32(const float* VA, const float* VB, const 
     for (int wi = 0; wi < NMI; ++wi) Hg[wi] += W[wi];
   }
   // phase 2: X += V W, two tiles interleaved (dependent-accumulator latency 40 > issue 32 cycles)
-  float b0[4 * NMI], b1[4 * NMI];
+  float c0[4 * NMI], c1[4 * NMI];
 #pragma unroll
   for (int mt = 0; mt < NMT; mt += 2) {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
-    ld_chunks<NMI>(b0, VB, mt, lane);
-    if (mt + 1 < NMT) ld_chunks<NMI>(b1, VB, mt + 1, lane);
+    ld2(c0, mt);
+    if (mt + 1 < NMT) ld2(c1, mt + 1);
 #pragma unroll
     for (int wi = 0; wi < NMI; ++wi)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        X[mt] = mfma16(b0[4 * wi + r], W[wi][r], X[mt]);
-        if (mt + 1 < NMT) X[mt + 1] = mfma16(b1[4 * wi + r], W[wi][r], X[mt + 1]);
+        X[mt] = mfma16(c0[4 * wi + r], W[wi][r], X[mt]);
+        if (mt + 1 < NMT) X[mt + 1] = mfma16(c1[4 * wi + r], W[wi][r], X[mt + 1]);
       }
     post.at(mt, X);  // the previous pair, behind this pair's MFMAs
   }
@@ -335,8 +368,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
         }
         FST(7);
         const float* img = reinterpret_cast<const float*>(lds + buf * BUF);
-        const float* VA = img;
-        const float* VB = img + G32::VA;
+        const float* VRp = img;
         const float* TPi = img + 2 * Img<B, float>::V;
         const int gd = g + 1 < NG ? g + 1 : has_next ? 0 : g, id = g + 1 < NG ? i : has_next ? inext : i;
         DmaJob<B, float> d{lds + (buf ^ 1) * BUF, vimg(id, gd), timg(id, gd), sflag};
@@ -363,9 +395,9 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
             if (pipe) {
               float* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
               const XPipe32<B> xp{xs.rs, uniform_rsrc(Xn + (size_t)col * ldm), xs.base};
-              apply32<B, true>(VA, VB, TPi, X, Hd, dh, xp);
+              apply32<B, true>(VRp, TPi, X, Hd, dh, xp);
             } else {
-              apply32<B, true>(VA, VB, TPi, X, Hd, dh);
+              apply32<B, true>(VRp, TPi, X, Hd, dh);
             }
             FST(13);
             if (!has_next)  // segment's last element: the group's head rows leave (write-through)
@@ -381,7 +413,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
             for (int mi = 0; mi < NMI; ++mi) Hd[NMT - NMI + mi] = tmp[mi];
             FST(2);
           } else {
-            apply32<B, false>(VA, VB, TPi, Hd, Hd, dh);
+            apply32<B, false>(VRp, TPi, Hd, Hd, dh);
             FST(13);
           }
         } else {

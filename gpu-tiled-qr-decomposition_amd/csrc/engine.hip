@@ -70,8 +70,8 @@ __device__ unsigned long long g_wst[4096 * 64];   // per-wave activity sums (flo
 namespace tqr {
 static_assert(FST_N <= 24, "g_fst holds 24 categories per workgroup");
 static_assert(Geo<256>::TPIMG == 1024 && Geo<16>::TPIMG == 256, "host tpimg_doubles mirrors Geo::TPIMG");
-static_assert(Img<256, float>::V == 8192 && Img<256, float>::T == 384 && Img<16, float>::V == 256 && Img<16, float>::T == 128 &&
-                  Img<64, float>::V == 2048 && Img<64, float>::T == 384,
+static_assert(Img<256, float>::V == 4096 && Img<256, float>::T == 384 && Img<16, float>::V == 128 && Img<16, float>::T == 128 &&
+                  Img<64, float>::V == 1024 && Img<64, float>::T == 384,
               "host wk_bytes mirrors Img<B, float>");
 static_assert(Geo<256>::TPK <= Geo<256>::TSZ && Geo<16>::TPK <= Geo<16>::TSZ, "packed T fits the Gram buffer");
 
@@ -564,10 +564,7 @@ static size_t tpimg_doubles(int b) {  // packed T image (Geo<b>::TPIMG)
   return (16 * nri * nri + 127) / 128 * 128;
 }
 // fp32 chain image slots (doubles; tiles.hpp Geo32 / Img<B, float>)
-static size_t vimg32_doubles(int b) {
-  const size_t nmi = (b < 32 ? b : 32) / 16;
-  return (size_t)(b / 16) * nmi * 256;  // (VA + VB) floats / 2
-}
+static size_t vimg32_doubles(int b) { return (size_t)b * (b < 32 ? b : 32) / 2; }  // VR floats / 2
 static size_t timg32_doubles(int b) {
   const size_t nmi = (b < 32 ? b : 32) / 16, npr = nmi * (nmi + 1) / 2;
   return (npr * 256 / 2 + 127) / 128 * 128;

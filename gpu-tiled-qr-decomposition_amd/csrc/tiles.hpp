@@ -89,18 +89,31 @@ struct Geo {
 };
 
 // fp32 chain geometry (chain32.hpp): v_mfma_f32_16x16x4_f32 tiles of 16 strip rows (NMT per tile)
-// and 16 reflectors (NMI per group). LDS / workspace images (floats, lane-major 16-B chunks):
-//   VA [mt][chunk < NMI][lane][4]  phase-1 A operands  V[16mt + 4x + r][16mi + y]
-//   VB [mt][wi  < NMI][lane][4]    phase-2 A operands  V[16mt + y][16wi + 4x + r]
+// and 16 reflectors (NMI per group). LDS / workspace images (floats):
+//   VR [row R < B][IB]  V, one layout read by both phases: reflector c = 16wi + 4x + r at
+//                       position 4NMI x + 4wi + r of its row (the 4 values a phase-2 lane needs
+//                       are one 16-B slot), 16-B slots XOR-swizzled by sw(R) (vr_sw) so that
+//                       phase 1's ds_read_b32 and phase 2's ds_read_b128 are conflict-free
 //   TP [pair (mi <= wi)][lane][4]  W = -T^T Z operands -T[16mi + 4x + r][16wi + y]
-// (lane = 16x + y; chunk of VA = (4r + ... see chain32.hpp); slots in doubles, whole KiB.
+// (lane = 16x + y); slots in doubles, whole KiB. (Round 2 had VA and VB, one layout per phase:
+// twice the LDS-DMA bytes.)
 template <int B>
 struct Geo32 {
   static constexpr int IB = Geo<B>::IB, NG = Geo<B>::NG;
   static constexpr int NMT = B / 16, NMI = IB / 16, NPR = NMI * (NMI + 1) / 2;
-  static constexpr int VA = NMT * NMI * 256, VB = VA, TP = NPR * 256;  // floats
-  static constexpr int VIMG = (VA + VB) / 2;                           // doubles (multiple of 128)
+  static constexpr int VR = B * IB, TP = NPR * 256;  // floats
+  static constexpr int VIMG = VR / 2;                // doubles (multiple of 128)
   static constexpr int TIMG = (TP / 2 + 127) / 128 * 128;
+  // slot swizzle of row R (IB = 32: found by exhaustive search over XOR maps of R's bits,
+  // conflict-free for both phases' lane groups; IB = 16: none)
+  __device__ static constexpr int vr_sw(int R) {
+    return IB == 32 ? ((((R >> 1) ^ (R >> 2)) & 1) | (((R >> 3) & 1) << 2)) : 0;
+  }
+  // float offset of V(R, c) in the image
+  __device__ static constexpr int vr_at(int R, int c) {
+    const int wi = c >> 4, x = (c >> 2) & 3, r = c & 3, p = 4 * NMI * x + 4 * wi + r;
+    return R * IB + (((p >> 2) ^ vr_sw(R)) << 2) + (p & 3);
+  }
 };
 // workspace slot sizes (doubles) of one reflector group's images, by storage type: fp64 storage
 // = the fp64 chain's V image + packed T; fp32 storage = the fp32 chain's VA/VB/TP images
