@@ -1453,6 +1453,8 @@ int tqr_tile_batch(int dtype, int type, int b, int nblocks, const void* V, int l
     return TQR_EINVAL;
   const int rows = type == DAPP ? 2 * b : b;  // rows of one block: [A; B] or C
   if (ldv < b || ldb < rows || (out && ldo < rows)) return TQR_EINVAL;
+  // the batch lives in one 2b-row device matrix addressed by 32-bit buffer offsets
+  if ((size_t)(dtype == TQR_F64 ? 8 : 4) * 2 * b * ((size_t)(1 + nblocks) * b) > 0x7fffffffull) return TQR_EINVAL;
   int st = check_device();
   if (st) return st;
   kfn kp, ku, kt;

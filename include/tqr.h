@@ -156,7 +156,8 @@ int tqr_tile_tsmqr(int dtype, const void* V, void* A, void* B, const void* tau, 
  *   type DAPP (TSMQR): V = b x b dense TSQRT V_B (ldv), tau = its b taus, blk = 2b x b [A; B] (ldb);
  *   type SAPP (UNMQR): V = b x b GEQRT tile (unit-lower V below the diagonal), blk = b x b C.
  * *ms = device time of the update launch (HIP events); out (optional) receives the nblocks
- * results, block j at out + j*b*ldo. */
+ * results, block j at out + j*b*ldo. The batch is one 2b-row device matrix of (1 + nblocks) b
+ * columns addressed with 32-bit offsets: more than 2^31 - 1 bytes returns TQR_EINVAL. */
 int tqr_tile_batch(int dtype, int type, int b, int nblocks, const void* V, int ldv, const void* tau,
                    const void* blk, int ldb, void* out, int ldo, float* ms);
 

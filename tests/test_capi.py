@@ -64,6 +64,9 @@ def test_invalid_engine_and_batch_args_without_gpu(tqr):
     # only the update types (SAPP = 1, DAPP = 3) batch; GEQRT (0) is rejected
     ms = ctypes.c_float()
     assert L.tqr_tile_batch(1, 0, 32, 4, None, 32, None, None, 64, None, 0, ctypes.byref(ms)) == -1
+    # a batch beyond the 32-bit offsets of its device matrix (fp64, b = 256: 2049 tiles, 2.15 GB)
+    z = ctypes.c_void_p(1)
+    assert L.tqr_tile_batch(1, 3, 256, 2048, z, 256, z, z, 512, None, 0, ctypes.byref(ms)) == -1
     assert L.tqr_dist_import(None, None, 0) == -1
     assert L.tqr_plan_execute(None, None, 0, None, None) == -1
 
