@@ -10,9 +10,10 @@ tqr.LIB_PATH = tqr.LIB_PATH.replace("libtqr.so", os.environ.get("TQR_FST_LIB", "
 L = tqr.lib()
 m = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 b = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-A = torch.empty((m, m), dtype=torch.float64, device="cuda")
-tau = torch.zeros((m // b, m), dtype=torch.float64, device="cuda")
-p = tqr.TiledQR(m, m, b, torch.float64)
+dt = torch.float32 if os.environ.get("TQR_FST_DTYPE") == "f32" else torch.float64
+A = torch.empty((m, m), dtype=dt, device="cuda")
+tau = torch.zeros((m // b, m), dtype=dt, device="cuda")
+p = tqr.TiledQR(m, m, b, dt)
 for rep in range(2):
     tqr.fill_randzo(A, m, m, 5)
     p.execute(A, tau)
@@ -36,7 +37,7 @@ chain = typ == 4
 print(f"{m}^2 b={b}: {n} tasks, launch span {e.max() / 1e3:.1f} ms, {grid.value} workgroups")
 print(" step  panel start..end (ms)   chains start..end (ms)   chain tasks")
 K = m // b
-for kk in list(range(0, K, 4)) + [K - 1]:
+for kk in list(range(0, K, max(1, K // 16))) + [K - 1]:
     pm = (k == kk) & ~chain
     cm = (k == kk) & chain
     ps = f"{s[pm].min() / 1e3:7.2f}..{e[pm].max() / 1e3:7.2f}" if pm.any() else "   -   "
