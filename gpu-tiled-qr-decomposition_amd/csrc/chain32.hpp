@@ -292,7 +292,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
     const bool head_in = ts && i == ifirst;  // first element of a later segment: head arrives per group
     {
       bool ok = true;
-      if (t == 0) {
+      if (t == FLOW_PT) {
         if (head_in) ok = spin_ge(&acg[0], seg, err);
         FST(9);
         if (ok && k > 0 && tc_pf < k) ok = spin_ge(tc(i), k, err);
@@ -333,7 +333,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
       for (int g = 0; g < NG; ++g) {
         {
           bool ok = true;
-          if (t == 0 && g + 1 == NG) {
+          if (t == FLOW_PT && g + 1 == NG) {
             // last group: may the next element's strip stream in during this phase 2? (its tile
             // must have received step k-1: Tc, loaded two groups ahead)
 #ifdef TQR_DIAG_NOSTRIP
@@ -342,7 +342,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
             sflag[44] = (NG > 1 && ts && has_next && (k == 0 || tc_pf >= k)) ? 1 : 0;
 #endif
           }
-          if (t == 0) {
+          if (t == FLOW_PT) {
             if (head_in && g + 1 < NG) ok = spin_ge(&acg[g + 1], seg, err);  // head rows of g+1 final
             if (ok) {
               if (g + 1 < NG) ok = ready(i, g + 1);
@@ -357,7 +357,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
           pending = nullptr;
         }
         if (!has_next && g > 0) publish_after_drain(&acg[g - 1], 1);
-        if (t == 0) {
+        if (t == FLOW_PT) {
           if (!remote) {
             pv.prefetch(rc, false);
           } else {

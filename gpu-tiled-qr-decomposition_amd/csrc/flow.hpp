@@ -106,6 +106,20 @@ constexpr int FLOW_NT = 512;
 constexpr int FLOW_NW = FLOW_NT / 64;      // waves
 constexpr int FLOW_SW = 16 * FLOW_NW;      // strip width (columns) of a chain task
 constexpr bool FLOW_PF = true;  // software-pipelined operand reads (also at 2 waves/SIMD)
+// The thread that polls a task's dependency counters, keeps the Rc view and writes the sync-point
+// verdicts (publishes stay with thread 0).
+#ifndef TQR_POLL_T
+#define TQR_POLL_T 0
+#endif
+constexpr int FLOW_PT = TQR_POLL_T;
+// The fp64 chain polls from wave 7: thread 0's wave also carries the publishes, and the waves'
+// stamps showed it the last to reach most group barriers (its partner and waves 1-3 waiting on
+// it); the upper waves, favoured in phase 1 (phase_prio), have slack. 130.6-130.9 ms against
+// 132.6-133.0 at 16384^2 (waves 4-7 alike; moving the publishes as well measured no better).
+#ifndef TQR_CHAIN_PT
+#define TQR_CHAIN_PT 448
+#endif
+constexpr int FLOW_CHAIN_PT = TQR_CHAIN_PT;  // the fp64 chain's poll thread
 constexpr unsigned long long FLOW_TIMEOUT = 500000000ull;  // 5 s of s_memrealtime (100 MHz)
 
 // Multi-GPU (tile-column cyclic partition, one process per GPU): peer buffers opened by IPC.
@@ -198,7 +212,7 @@ __device__ __forceinline__ int lds_ld_volatile(int* p) { return *(volatile lds_i
 
 // all threads: thread 0's verdict (after its polls)
 __device__ __forceinline__ bool wg_verdict(bool ok0, int* sflag) {
-  if (threadIdx.x == 0) *lds_int(sflag) = ok0 ? 1 : 0;
+  if (threadIdx.x == FLOW_PT) *lds_int(sflag) = ok0 ? 1 : 0;
   __syncthreads();
   const bool ok = lds_ld_volatile(sflag) != 0;
   __syncthreads();
@@ -289,11 +303,11 @@ struct DmaJob {
 // FLAT: the verdict read as a generic (flat) load — its wait is vmcnt(0), i.e. a full drain, which
 // only the fp32 chain still uses (its register allocation spills in the phase loops otherwise;
 // every sync point there drains fully anyway).
-template <bool DRAIN, bool FLAT = false>
+template <bool DRAIN, bool FLAT = false, int PT = FLOW_PT>
 __device__ __forceinline__ bool sync_point(bool ok0, int* sflag, int& par) {
   int* slot = sflag + 40 + par;  // LDS tail (ints from the task word): [task][flag][..][verdicts 41,42][..][Rc view 49..][..][FST sums 64..]
   par ^= 1;
-  if (threadIdx.x == 0) *lds_int(slot) = ok0 ? 1 : 0;
+  if (threadIdx.x == PT) *lds_int(slot) = ok0 ? 1 : 0;
   WST_T0();
   if (DRAIN) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -309,11 +323,11 @@ __device__ __forceinline__ bool sync_point(bool ok0, int* sflag, int& par) {
 // previous group's head-row stores and this group's head-row loads, issued after that DMA — may
 // still be in flight (the stores are read back by this workgroup only, the loads are waited for
 // at their first use).
-template <int N>
+template <int N, int PT = FLOW_PT>
 __device__ __forceinline__ bool sync_point_cnt(bool ok0, int* sflag, int& par) {
   int* slot = sflag + 40 + par;
   par ^= 1;
-  if (threadIdx.x == 0) *lds_int(slot) = ok0 ? 1 : 0;
+  if (threadIdx.x == PT) *lds_int(slot) = ok0 ? 1 : 0;
   static_assert(N >= 0 && N < 64, "vmcnt range");
   WST_T0();
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
@@ -328,11 +342,11 @@ __device__ __forceinline__ bool sync_point_cnt(bool ok0, int* sflag, int& par) {
 // loads issued after them need not be — phase 1 waits for each strip row as it reaches it (the
 // compiler's vmcnt per use; the LDS-DMA of the next group, issued in between, only makes those
 // waits conservative). A wave without loads (strip past the tile) drains fully.
-template <int NX>
+template <int NX, int PT = FLOW_PT>
 __device__ __forceinline__ bool sync_point_first(bool ok0, int* sflag, int& par, bool loaded) {
   int* slot = sflag + 40 + par;
   par ^= 1;
-  if (threadIdx.x == 0) *lds_int(slot) = ok0 ? 1 : 0;
+  if (threadIdx.x == PT) *lds_int(slot) = ok0 ? 1 : 0;
   static_assert(NX >= 0 && NX < 64, "vmcnt range");
   WST_T0();
   if (loaded) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NX) : "memory");
@@ -348,15 +362,16 @@ __device__ __forceinline__ void publish_after_drain(int* p, int delta) {
   if (threadIdx.x == 0) __hip_atomic_fetch_add(gptr(p), delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Thread 0's view of one panel's group counters Rc[k][0..NG): rv[g] (LDS, thread 0 only) holds
-// an observed value, so the V/T images of any member < rv[g] of group g may be LDS-DMA'd.
+// The poll thread's view of one panel's group counters Rc[k][0..NG): rv[g] (LDS) holds an
+// observed value, so the V/T images of any member < rv[g] of group g may be LDS-DMA'd.
 // ensure(g, need) re-reads the row (one round trip) only when rv[g] < need. No acquire fence:
 // the images are write-once inside a launch (one producer, stored sc1 and drained before its
 // counter add), no workgroup reads a slot before observing its counter, and the DMA itself is
 // an sc1 (L1-bypassing) load — so no CU can hold a stale copy of an image line.
-// prefetch() (thread 0, right after a sync point) issues the row's loads early, so that the next
-// ensure() normally finds fresh values without an exposed round trip.
-template <int NG>
+// prefetch() (the poll thread, right after a sync point) issues the row's loads early, so that
+// the next ensure() normally finds fresh values without an exposed round trip. (Staging the row
+// into LDS by LDS-DMA instead, no registers held: 132.5 ms against 130.6-130.9 at 16384^2.)
+template <int NG, int PT = FLOW_PT>
 struct PanelView {
   lds_int_t* rv;
   int pf[NG];
@@ -364,7 +379,7 @@ struct PanelView {
   __device__ __forceinline__ void init(int* lds_words) {
     rv = lds_int(lds_words);
     pf_valid = false;
-    if (threadIdx.x == 0)
+    if (threadIdx.x == PT)
       for (int g = 0; g < NG; ++g) rv[g] = 0;
   }
   __device__ __forceinline__ void prefetch(int* rc, bool sys) {
@@ -449,7 +464,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
   // the tile(s) must have received step k-1 on every strip
   {
     bool ok = true;
-    if (t == 0 && k > 0)
+    if (t == FLOW_PT && k > 0)
       for (int s = 0; s < a.ns && ok; ++s) ok = spin_ge(&a.Tc[((size_t)(qrs ? k : l) * a.q + k) * a.ns + s], k, a.err);
     if (!wg_verdict(ok, sflag)) return;
   }
@@ -460,7 +475,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     const int c0 = g * IB, ks0 = c0 / 4;
     if (!qrs) {  // R_kk rows of group g as left by the previous chain member
       FST(10);
-      const bool ok = t == 0 ? spin_ge(&a.Rr[(size_t)k * NG + g], pos, a.err) : true;
+      const bool ok = t == FLOW_PT ? spin_ge(&a.Rr[(size_t)k * NG + g], pos, a.err) : true;
       if (!wg_verdict(ok, sflag)) return;
       FST(1);
     }
@@ -541,7 +556,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     wg_publish(&a.Rc[(size_t)k * NG + g], 1);
     FST(10);
     if (!qrs) {  // R_kk head rows right of the group as left by the previous member's trailing
-      const bool ok = t == 0 ? spin_ge(&a.Rt[(size_t)k * NG + g], pos, a.err) : true;
+      const bool ok = t == FLOW_PT ? spin_ge(&a.Rt[(size_t)k * NG + g], pos, a.err) : true;
       if (!wg_verdict(ok, sflag)) return;
       FST(1);
     }
@@ -593,7 +608,7 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
   const int t = threadIdx.x, pos = i - k;
   for (int g = 0; g < NG; ++g) {
     bool ok = true;
-    if (t == 0) ok = spin_ge(&a.Rc[(size_t)k * NG + g], pos + 1, a.err);
+    if (t == FLOW_PT) ok = spin_ge(&a.Rc[(size_t)k * NG + g], pos + 1, a.err);
     if (!wg_verdict(ok, sflag)) return;
     const size_t vo = flow_vw_off<B, S>(a.p, i, k, g), to = flow_tw_off<B, S>(a.p, i, k, g);
     const __amdgpu_buffer_rsrc_t vsrc = uniform_rsrc(a.Wk[k] + vo), tsrc = uniform_rsrc(a.Wk[k] + to);
@@ -671,6 +686,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   S* A = (S*)a.A;
   const size_t ldm = a.ldm;
   const int t = threadIdx.x, w = t >> 6;
+  constexpr int PT = FLOW_CHAIN_PT;
   const int col = s * FLOW_SW + 16 * w;  // this wave's 16 columns inside the tile
   const bool active = B % FLOW_SW == 0 || col < B;  // (compile-time true unless B < FLOW_SW)
   S* At = A + (size_t)j * B * ldm + (size_t)k * B;  // tile (k,j): the chain's head rows
@@ -691,9 +707,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   int buf = 0, par = 0;
   int* pending = nullptr;
   bool dma_next = false;  // group 0 of the next element already in flight
-  PanelView<NG> pv;
+  PanelView<NG, PT> pv;
   pv.init(sflag + 48);
-  int tc_pf = -1;  // thread 0: Tc of the next element's tile, loaded two groups ahead
+  int tc_pf = -1;  // poll thread: Tc of the next element's tile, loaded two groups ahead
   bool xin = false;  // this element's strip was loaded during the previous element's last phase 2
   // multi-GPU, panel owned by another rank: per-member flags forwarded by the owner
   const bool remote = a.dist && (k % a.world != a.rank);
@@ -712,7 +728,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     const bool ts = i != k;
     {
       bool ok = true;
-      if (t == 0) {
+      if (t == PT) {
         if (i == ifirst && seg > 0) ok = spin_ge(&acg[0], seg, err);
         FST(9);
         if (ok && k > 0 && tc_pf < k) ok = spin_ge(tc(i), k, err);
@@ -721,7 +737,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         if (ok && !dma_next) ok = ready(i, 0);
       }
       FST(j == k + 1 ? 18 : 19);  // Rc wait at element start (lookahead column / other)
-      if (!sync_point<false>(ok, sflag, par)) return;
+      if (!sync_point<false, false, PT>(ok, sflag, par)) return;
     }
     FST(7);
     S* Xt = ts ? A + (size_t)j * B * ldm + (size_t)i * B : At;
@@ -758,7 +774,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         FST(g == 0 ? 22 : 21);
 #endif
-        if (t == 0 && g + 1 == NG) {
+        if (t == PT && g + 1 == NG) {
           // last group: may the next element's strip stream in during this phase 2? (its tile
           // must have received step k-1: Tc, loaded two groups ahead)
 #ifdef TQR_DIAG_NOSTRIP
@@ -767,7 +783,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
           sflag[44] = (NG > 1 && has_next && (k == 0 || tc_pf >= k)) ? 1 : 0;
 #endif
         }
-        if (t == 0) {
+        if (t == PT) {
           // first element of a later segment: head rows of group g+1 (prefetched below) final?
           if (i == ifirst && seg > 0 && g + 1 < NG) ok = spin_ge(&acg[g + 1], seg, err);
           if (ok) {
@@ -783,8 +799,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         const bool full = !has_next || (xin && g == 1);
         WMARK(2);
         constexpr int NH = FLOW_PF ? 2 * G::NRI : G::NRI;  // head stores + next head loads
-        if (!(g == 0 ? sync_point_first<NX>(ok, sflag, par, active)
-                     : full ? sync_point<true>(ok, sflag, par) : sync_point_cnt<NH>(ok, sflag, par)))
+        if (!(g == 0 ? sync_point_first<NX, PT>(ok, sflag, par, active)
+                     : full ? sync_point<true, false, PT>(ok, sflag, par) : sync_point_cnt<NH, PT>(ok, sflag, par)))
           return false;
 #ifdef TQR_FLOW_STAMPS
         wt_ = __builtin_amdgcn_s_memrealtime();  // (the sync point's own time is in slots 0, 1)
@@ -801,7 +817,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       }
       // segment's last element: its head rows of group g-1 (stored write-through) are drained
       if (!has_next && g > 0) publish_after_drain(&acg[g - 1], 1);
-      if (t == 0) {  // early loads of the counters the next sync point will test
+      if (t == PT) {  // early loads of the counters the next sync point will test
         if (!remote) {
           pv.prefetch(rc, false);
         } else {
@@ -878,7 +894,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     FST(4);
   }
   // last element's strip and its last head-row group: drain, then publish both
-  sync_point<true>(true, sflag, par);
+  sync_point<true, false, PT>(true, sflag, par);
   if (pending) publish_after_drain(pending, 1);
   publish_after_drain(&acg[NG - 1], 1);
   FST(4);
