@@ -1,11 +1,13 @@
+# w32 (one wave per SIMD) with the 32-column panel trailing update: parity subset, bench, stamps of both forms
 set -o pipefail
-mkdir -p gpurun_out/r02_c21
-timeout -k 10 400 python -u -m pytest tests -q -x -m gpu --timeout 300 --timeout-method thread -k "f32 or fp32 or float32" > gpurun_out/r02_c21/pytest_f32.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/r02_c21/pytest_f32.log; exit 1; }
-tail -1 gpurun_out/r02_c21/pytest_f32.log
-timeout -k 10 200 python bench.py --no-cpu-baseline --no-host-api --steps 5 --warmup 2 --storage f32 --rows 32768 --cols 32768 > gpurun_out/r02_c21/bench_f32.json 2> gpurun_out/r02_c21/bench_f32.err || { echo bench failed; tail gpurun_out/r02_c21/bench_f32.err; exit 1; }
-python3 -c "import json;d=json.loads(open('gpurun_out/r02_c21/bench_f32.json').read());print(d['ms_per_step'], d['roofline']['frac'])"
-for v in fst; do
-  echo "== $v"
-  TQR_FST_LIB=libtqr_$v.so TQR_FST_DTYPE=f32 timeout -k 10 200 python tools/flowstamps.py 32768 > gpurun_out/r02_c21/fst_$v.txt 2>&1 || { echo "fst $v failed"; tail gpurun_out/r02_c21/fst_$v.txt; exit 1; }
-  grep -E "wall|phase|store|Rc wait in-elem other|strip|drain" gpurun_out/r02_c21/fst_$v.txt
+OUT=gpurun_out/c21; mkdir -p $OUT
+export TMPDIR=/tmp
+TQR_LIB=libtqr_w32.so timeout -k 10 300 python -u -m pytest tests/test_gpu_factor.py -q -x -m gpu --timeout 120 --timeout-method thread -k "vs_oracle or vs_reference or structured" > $OUT/pytest_w32.log 2>&1 || { echo "pytest w32 failed"; tail -30 $OUT/pytest_w32.log; exit 1; }
+tail -2 $OUT/pytest_w32.log
+for L in libtqr.so libtqr_w32.so; do
+  TQR_LIB=$L timeout -k 10 120 python bench.py --no-cpu-baseline --no-host-api --steps 10 --warmup 2 > $OUT/bench_${L}.json 2> $OUT/bench_${L}.err || { echo "bench $L failed"; tail -20 $OUT/bench_${L}.err; exit 1; }
+  echo "$L $(python3 -c "import json,sys; d=json.load(open('$OUT/bench_${L}.json')); print(d['ms_per_step'], d['value'], d['roofline']['frac'])")"
+done
+for F in libtqr_fst.so libtqr_diag_w32.so; do
+  TQR_FST_LIB=$F timeout -k 10 120 python tools/flowstamps.py 16384 > $OUT/fst_$F.txt 2>&1 || { echo "stamps $F failed"; tail -20 $OUT/fst_$F.txt; exit 1; }
 done
