@@ -1102,7 +1102,7 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     // multi-GPU: counters and flags are reset by tqr_dist_reset (all ranks, then a barrier)
     if (pl->world == 1) HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
     if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
-    hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(pl->dtype == TQR_F64 ? flow_nt<double>() : flow_nt<float>()), pl->ldsF, cs, f);
+    hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(FLOW_NT), pl->ldsF, cs, f);
     HIPCHK(hipGetLastError());
     if (pl->profile) {
       HIPCHK(hipEventRecord(pl->ev1, cs));

@@ -120,17 +120,6 @@ constexpr int FLOW_PT = TQR_POLL_T;
 #define TQR_CHAIN_PT 448
 #endif
 constexpr int FLOW_CHAIN_PT = TQR_CHAIN_PT;  // the fp64 chain's poll thread
-// Workgroup size of k_flow by storage type. fp32 keeps 8 waves (FLOW_NT). fp64 with
-// TQR_NT64 = 256 runs ONE wave per SIMD with the whole 512-register file: each wave owns 32
-// columns of the 128-column strip (two 16-column groups sharing every LDS operand read), and the
-// pair arbitration of two waves per SIMD is gone.
-#ifndef TQR_NT64
-#define TQR_NT64 512
-#endif
-template <typename S>
-__host__ __device__ constexpr int flow_nt() { return sizeof(S) == 8 ? TQR_NT64 : FLOW_NT; }
-template <typename S>
-__host__ __device__ constexpr int flow_chain_pt() { return flow_nt<S>() == 512 ? FLOW_CHAIN_PT : flow_nt<S>() - 64; }
 constexpr unsigned long long FLOW_TIMEOUT = 500000000ull;  // 5 s of s_memrealtime (100 MHz)
 
 // Multi-GPU (tile-column cyclic partition, one process per GPU): peer buffers opened by IPC.
@@ -273,8 +262,7 @@ template <int B, typename S = double>
 struct DmaJob {
   static constexpr int VIMG = Img<B, S>::V;
   static constexpr int NIV = Img<B, S>::V / 128, NIT = Img<B, S>::T / 128;
-  static constexpr int NW = flow_nt<S>() / 64;
-  static constexpr int PV = (NIV + NW - 1) / NW, PT = (NIT + NW - 1) / NW;
+  static constexpr int PV = (NIV + FLOW_NW - 1) / FLOW_NW, PT = (NIT + FLOW_NW - 1) / FLOW_NW;
   static constexpr int STEPS = PV + PT;
   double* dst;
   const double* v;
@@ -289,10 +277,10 @@ struct DmaJob {
     // wave id made provably uniform: addresses = scalar base + one per-lane offset register
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (m < PV) {
-      const int u = min(w + NW * m, NIV - 1);
+      const int u = min(w + FLOW_NW * m, NIV - 1);
       dma16(v + u * 128 + 2 * lane, dst + u * 128);
     } else if (m < STEPS) {
-      const int u = min(w + NW * (m - PV), NIT - 1);
+      const int u = min(w + FLOW_NW * (m - PV), NIT - 1);
       dma16(t + u * 128 + 2 * lane, dst + VIMG + u * 128);
     }
   }
@@ -456,7 +444,7 @@ __device__ __noinline__ void write_images32(const double* Vs, const double* Ts, 
 template <int B, typename S>
 __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* lds, int* sflag) {
   using G = Geo<B>;
-  constexpr int IB = G::IB, VP = G::VP, TP = G::TP, NG = G::NG, NT = flow_nt<S>();
+  constexpr int IB = G::IB, VP = G::VP, TP = G::TP, NG = G::NG;
   double* Vs = lds;
   double* Hs = Vs + G::VSZ;
   double* Ts = Hs + G::TSZ;
@@ -495,7 +483,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt + (size_t)c0 * ldm);  // offsets span IB columns
       const int rlo = qrs ? c0 : 0;
 #pragma unroll 4
-      for (int idx = t; idx < B * IB / 2; idx += NT) {
+      for (int idx = t; idx < B * IB / 2; idx += FLOW_NT) {
         const int r = 2 * (idx % (B / 2)), c = idx / (B / 2);
         double v0 = 0.0, v1 = 0.0;
         if (r >= rlo) ld_pair<S>(rs, (unsigned)(((size_t)c * ldm + r) * sizeof(S)), v0, v1);
@@ -504,7 +492,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       }
     }
     if (!qrs) {
-      for (int idx = t; idx < IB * IB; idx += NT) {
+      for (int idx = t; idx < IB * IB; idx += FLOW_NT) {
         const int r = idx % IB, c = idx / IB;
         if (r <= c) Hs[r * TP + c] = ldc(Rt + (size_t)(c0 + c) * ldm + c0 + r);
       }
@@ -522,7 +510,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt + (size_t)c0 * ldm);
       const int rlo = qrs ? c0 : 0;
 #pragma unroll 4
-      for (int idx = t; idx < B * IB / 2; idx += NT) {
+      for (int idx = t; idx < B * IB / 2; idx += FLOW_NT) {
         const int r = 2 * (idx % (B / 2)), c = idx / (B / 2);
         if (r >= rlo)
           st_pair<S>(rs, (unsigned)(((size_t)c * ldm + r) * sizeof(S)), Vs[vimg_inv(r) * VP + G::pc(c)],
@@ -530,7 +518,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       }
     }
     if (!qrs) {
-      for (int idx = t; idx < IB * IB; idx += NT) {
+      for (int idx = t; idx < IB * IB; idx += FLOW_NT) {
         const int r = idx % IB, c = idx / IB;
         if (r <= c) st(Rt + (size_t)(c0 + c) * ldm + c0 + r, Hs[r * TP + c]);
       }
@@ -538,7 +526,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     if (t < IB) st(tau + (size_t)k * a.m + (size_t)(qrs ? k : l) * B + c0 + t, tauv[t]);
     wg_publish(&a.Rr[(size_t)k * NG + g], 1);  // includes the drain and the barrier
     if (qrs) {
-      for (int idx = t; idx < B * IB; idx += NT) {
+      for (int idx = t; idx < B * IB; idx += FLOW_NT) {
         const int r = idx % B, c = idx / B, d = c0 + c;
         if (r <= d) Vs[vimg_inv(r) * VP + G::pc(c)] = r == d ? 1.0 : 0.0;
       }
@@ -550,7 +538,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
 #endif
     // packed T (the Gram buffer is free now): the trailing update's and the chains' T operand
     double* Tp = Gs;
-    pack_t<B, NT>(Ts, Tp);
+    pack_t<B, FLOW_NT>(Ts, Tp);
     __syncthreads();
     FST(11);
     {  // V image (explicit) and packed T image of this group for the chains (LDS-DMA sources)
@@ -558,8 +546,8 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       double* vg = flow_vw<B, S>(a, qrs ? k : l, k, g);
       const __amdgpu_buffer_rsrc_t rv = uniform_rsrc(vg), rt = uniform_rsrc(tg);
       if constexpr (sizeof(S) == 8) {
-        for (int idx = t; idx < G::TPIMG / 2; idx += NT) st_pair<double>(rt, 16 * idx, Tp[2 * idx], Tp[2 * idx + 1]);
-        for (int idx = t; idx < G::VSZ / 2; idx += NT) st_pair<double>(rv, 16 * idx, Vs[2 * idx], Vs[2 * idx + 1]);
+        for (int idx = t; idx < G::TPIMG / 2; idx += FLOW_NT) st_pair<double>(rt, 16 * idx, Tp[2 * idx], Tp[2 * idx + 1]);
+        for (int idx = t; idx < G::VSZ / 2; idx += FLOW_NT) st_pair<double>(rv, 16 * idx, Vs[2 * idx], Vs[2 * idx + 1]);
       } else {
         write_images32<B>(Vs, Ts, rv, rt);  // the fp32 chain's operand images (chain32.hpp)
       }
@@ -580,34 +568,11 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     // updating meanwhile); the head resource is empty for GEQRT (loads 0, stores dropped) —
     // see flow_chain's UNMQR element.
     const int h0 = qrs ? c0 / 8 : 0;
-    constexpr int PNC = NT == 256 && B >= 128 ? 2 : 1;  // 16-column groups per wave
 #ifdef TQR_DIAG_NOPTRAIL  // what-if: no in-tile trailing update (results wrong)
-    for (int s = nstr; s < nstr; s += NT / 64) {
+    for (int s = nstr; s < nstr; s += FLOW_NT / 64) {
 #else
-    for (int s = w; s < nstr; s += NT / 64) {
+    for (int s = w; s < nstr; s += FLOW_NT / 64) {
 #endif
-      if constexpr (PNC > 1) {  // one wave per SIMD: 32-column strips, as the chains
-        if (PNC * s >= nstr) break;
-        const int col = c0 + IB + 16 * PNC * s;
-        const unsigned so = head_off<B, S>(ldm, c0);
-        double X2[PNC][G::NKS], H2[PNC][G::NRI], W2[PNC][G::NRI];
-        __amdgpu_buffer_rsrc_t rsH[PNC];
-        for (int c = 0; c < PNC; ++c) {
-          rsH[c] = head_rsrc(Rt + (size_t)(col + 16 * c) * ldm, !qrs);
-          load_strip_pair<B, S>(X2[c], Bt, ldm, col + 16 * c, h0);
-          load_head_buf<B, S, 16>(H2[c], rsH[c], so);
-        }
-        FST(16);
-        chain_zw<B, PNC>(Vs, Tp, X2, H2, W2, NoHook());
-        chain_x4<B, PNC>(Vs, X2, W2, NoPost());
-        FST(12);
-        for (int c = 0; c < PNC; ++c) {
-          store_strip_pair<B, S>(X2[c], Bt, ldm, col + 16 * c, h0);
-          store_head_buf<B, S, 16>(H2[c], rsH[c], so);
-        }
-        FST(17);
-        continue;
-      }
       asm volatile("" ::: "memory");
       const int col = c0 + IB + 16 * s;
       const __amdgpu_buffer_rsrc_t rsH = head_rsrc(Rt + (size_t)col * ldm, !qrs);
@@ -639,7 +604,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
 template <int B, typename S>
 __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sflag) {
   using G = Geo<B>;
-  constexpr int NG = G::NG, NT = flow_nt<S>();
+  constexpr int NG = G::NG;
   const int t = threadIdx.x, pos = i - k;
   for (int g = 0; g < NG; ++g) {
     bool ok = true;
@@ -651,9 +616,9 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
       if (r == a.rank) continue;
       double* pw = a.peers[r].Wk[k];
       const __amdgpu_buffer_rsrc_t vdst = uniform_rsrc(pw + vo), tdst = uniform_rsrc(pw + to);
-      for (int c = t; c < Img<B, S>::V / 2; c += NT)
+      for (int c = t; c < Img<B, S>::V / 2; c += FLOW_NT)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(vsrc, 16 * c, 0, 16), vdst, 16 * c, 0, 17);
-      for (int c = t; c < Img<B, S>::T / 2; c += NT)
+      for (int c = t; c < Img<B, S>::T / 2; c += FLOW_NT)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(tsrc, 16 * c, 0, 16), tdst, 16 * c, 0, 17);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -675,10 +640,8 @@ __device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sfla
 // barrier while its partner ran alone, every dependency and LDS bubble of a single wave exposed
 // (stamps: waves 1-3 waited 44 ms per workgroup at the barriers, waves 5-7 11 ms). Phase 1
 // favours the upper waves, phase 2 the lower ones, so the pair ends its group together.
-template <int NW>
 __device__ __forceinline__ void phase_prio(bool phase2) {
 #ifndef TQR_NO_PRIO
-  if constexpr (NW < 8) return;  // one wave per SIMD: nothing to arbitrate
   const bool upper = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4;
   if (upper != phase2) __builtin_amdgcn_s_setprio(1);
   else __builtin_amdgcn_s_setprio(0);
@@ -703,24 +666,6 @@ struct XPipe {
   }
   __device__ __forceinline__ void fin(double (&X)[Geo<B>::NKS]) const { xfer(Geo<B>::NKS / 2 - 1, X); }
 };
-// the same for NC 16-column groups per wave (chain_x4)
-template <int B, typename S, int NC>
-struct XPipeN {
-  __amdgpu_buffer_rsrc_t out[NC], in[NC];
-  unsigned base;
-  __device__ __forceinline__ void xfer(int h, double (&X)[NC][Geo<B>::NKS]) const {
-    const unsigned so = base + 8 * h * sizeof(S);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      st_pair<S, TQR_STRIP_ST_AUX>(out[c], so, X[c][2 * h], X[c][2 * h + 1]);
-      ld_pair<S, TQR_STRIP_LD_AUX>(in[c], so, X[c][2 * h], X[c][2 * h + 1]);
-    }
-  }
-  __device__ __forceinline__ void at(int h, double (&X)[NC][Geo<B>::NKS]) const {
-    if (h >= 1) xfer(h - 1, X);
-  }
-  __device__ __forceinline__ void fin(double (&X)[NC][Geo<B>::NKS]) const { xfer(Geo<B>::NKS / 2 - 1, X); }
-};
 
 // Elements: UNMQR(k,j) (segment 0 only, GE-type, the strip of tile (k,j) is X) and TSMQR(i,j,k)
 // for i in [i0,i1) (TS-type: X = strip of tile (i,j), head rows = strip of tile (k,j), group by
@@ -741,12 +686,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   S* A = (S*)a.A;
   const size_t ldm = a.ldm;
   const int t = threadIdx.x, w = t >> 6;
-  constexpr int PT = flow_chain_pt<S>(), NW = flow_nt<S>() / 64;
-  // 16-column groups per wave: 1 at 8 waves; 2 at one wave per SIMD (TQR_NT64 = 256) when the
-  // tile is wider than 4 x 16 columns (a 128-column strip = 4 waves x 32 columns)
-  constexpr int NC = 16 * NW >= B ? 1 : FLOW_SW / (16 * NW);
-  static_assert(NC * 16 * NW == FLOW_SW || 16 * NW >= B, "a chain task covers its strip");
-  const int col = s * FLOW_SW + 16 * NC * w;  // this wave's first column inside the tile
+  constexpr int PT = FLOW_CHAIN_PT;
+  const int col = s * FLOW_SW + 16 * w;  // this wave's 16 columns inside the tile
   const bool active = B % FLOW_SW == 0 || col < B;  // (compile-time true unless B < FLOW_SW)
   S* At = A + (size_t)j * B * ldm + (size_t)k * B;  // tile (k,j): the chain's head rows
   // everything the group loop needs from FlowArgs, read once per task: the asm memory clobbers
@@ -761,8 +702,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   int* const rc = &a.Rc[(size_t)k * NG];
   int* const acg = &a.Ac[(((size_t)k * Q + j) * NS + s) * NG];  // per head-row group
   auto tc = [&](int i) { return &Tc[((size_t)i * Q + j) * NS + s]; };
-  double X[NC][G::NKS];
-  double H[NC][G::NRI], Hn[NC][G::NRI], W[NC][G::NRI];
+  double X[G::NKS];
+  double H[G::NRI], Hn[G::NRI], W[G::NRI];
   int buf = 0, par = 0;
   int* pending = nullptr;
   bool dma_next = false;  // group 0 of the next element already in flight
@@ -806,8 +747,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     }
     dma_next = false;
 #ifndef TQR_DIAG_NOSTRIP
-    if (active && !xin)
-      for (int c = 0; c < NC; ++c) load_strip_pair<B, S>(X[c], Xt, ldm, col + 16 * c);
+    if (active && !xin) load_strip_pair<B, S>(X, Xt, ldm, col);
 #endif
     // head rows: written by another workgroup before this segment or by this one (sc1 loads
     // for both). The UNMQR element (i == k, GE-type V) runs the very same TSMQR code with a zero
@@ -815,11 +755,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     // are exactly the GE update (the zero rows add exact zeros) — one MFMA stream for both
     // element types keeps the register allocation of the hot TSMQR path clean (a separate GE
     // variant with ks0-skipping cost the TSMQR phase 2 its operand prefetch), for ~1 % extra flops.
-    __amdgpu_buffer_rsrc_t hrs[NC];  // UNMQR: empty resources, head = 0
-    for (int c = 0; c < NC; ++c) hrs[c] = head_rsrc(At + (size_t)(col + 16 * c) * ldm, ts);
+    const __amdgpu_buffer_rsrc_t hrs = head_rsrc(At + (size_t)col * ldm, ts);  // UNMQR: empty resource, head = 0
     const unsigned hoff = head_off<B, S>(ldm, 0);
-    if (FLOW_PF && active)
-      for (int c = 0; c < NC; ++c) load_head_buf<B, S, 16>(H[c], hrs[c], hoff);
+    if (FLOW_PF && active) load_head_buf<B, S, 16>(H, hrs, hoff);
     FST(4);
     const int inext = (i == k) ? i0 : i + 1;
     const bool has_next = inext < i1;
@@ -855,14 +793,12 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         }
         FST(j == k + 1 ? 20 : 0);  // Rc wait inside an element (lookahead column / other)
         // group 0: the strip / head loads of this element may still be in flight
-        // (with NC = 2 they exceed the 6-bit counter: waiting for all but the youngest 63 still
-        // covers everything older than them)
-        constexpr int NX = NC * (G::NKS / 2 + (FLOW_PF ? G::NRI : 0)) < 63 ? NC * (G::NKS / 2 + (FLOW_PF ? G::NRI : 0)) : 63;
+        constexpr int NX = G::NKS / 2 + (FLOW_PF ? G::NRI : 0);
         // full drain where a publish follows: the segment's last element (head rows, Ac) and the
         // first group after a streamed hand-over (the previous element's strip stores, Tc)
         const bool full = !has_next || (xin && g == 1);
         WMARK(2);
-        constexpr int NH = NC * (FLOW_PF ? 2 * G::NRI : G::NRI);  // head stores + next head loads
+        constexpr int NH = FLOW_PF ? 2 * G::NRI : G::NRI;  // head stores + next head loads
         if (!(g == 0 ? sync_point_first<NX, PT>(ok, sflag, par, active)
                      : full ? sync_point<true, false, PT>(ok, sflag, par) : sync_point_cnt<NH, PT>(ok, sflag, par)))
           return false;
@@ -891,8 +827,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         if (g + 2 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
       }
       FST(7);
-      if (!FLOW_PF && active)
-        for (int c = 0; c < NC; ++c) load_head_buf<B, S, 16>(H[c], hrs[c], hoff + g * IB * sizeof(S));
+      if (!FLOW_PF && active) load_head_buf<B, S, 16>(H, hrs, hoff + g * IB * sizeof(S));  // 2 waves/SIMD
       const double* Vs = lds + buf * BUF;
       const double* Ts = Vs + G::VIMG;
       // the other buffer is free (every wave passed this sync point): next DMA rides phase 1
@@ -906,17 +841,12 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       d.t = timg(k, 0);
 #endif
 #ifdef TQR_DIAG_NODMA  // what-if: no staging at all
-      if (active) {
-        if constexpr (NC == 1) apply_zw<B, true, NoHook, FLOW_PF, true>(Vs, Ts, X[0], H[0], W[0], 0);
-        else chain_zw<B, NC>(Vs, Ts, X, H, W, NoHook());
-      }
+      if (active) apply_zw<B, true, NoHook, FLOW_PF, true>(Vs, Ts, X, H, W, 0);
 #else
-      phase_prio<NW>(false);
+      phase_prio(false);
       WMARK(3);
-      if (active) {
-        if constexpr (NC == 1) apply_zw<B, true, DmaJob<B>, FLOW_PF, true>(Vs, Ts, X[0], H[0], W[0], 0, d);
-        else chain_zw<B, NC>(Vs, Ts, X, H, W, d);
-      } else
+      if (active) apply_zw<B, true, DmaJob<B>, FLOW_PF, true>(Vs, Ts, X, H, W, 0, d);
+      else
         for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
 #endif
       FST(15);
@@ -926,41 +856,23 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         // head rows stay with this workgroup inside the segment (plain write-back stores); the
         // segment's last element hands them to the next segment group by group: write-through
         // stores, drained, then Ac[k][j][s][g]++ (one group later, after the next drain)
-        for (int c = 0; c < NC; ++c) {
-          if (has_next) store_head_buf<B, S, 0>(H[c], hrs[c], hoff + g * IB * sizeof(S));
-          else store_head_buf<B, S, 16>(H[c], hrs[c], hoff + g * IB * sizeof(S));
-        }
+        if (has_next) store_head_buf<B, S, 0>(H, hrs, hoff + g * IB * sizeof(S));
+        else store_head_buf<B, S, 16>(H, hrs, hoff + g * IB * sizeof(S));
         FST(2);
-        if (FLOW_PF && g + 1 < NG)
-          for (int c = 0; c < NC; ++c) load_head_buf<B, S, 16>(Hn[c], hrs[c], hoff + (g + 1) * IB * sizeof(S));
+        if (FLOW_PF && g + 1 < NG) load_head_buf<B, S, 16>(Hn, hrs, hoff + (g + 1) * IB * sizeof(S));
       }
 #endif
       FST(14);
       WMARK(5);
-      phase_prio<NW>(true);
+      phase_prio(true);
       if (active) {
-        const unsigned xbase = (unsigned)((((size_t)(t & 15)) * ldm + 2 * ((t & 63) >> 4)) * sizeof(S));
-        if constexpr (NC == 1) {
-          if (pipe) {
-            S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
-            const XPipe<B, S> xp{uniform_rsrc(Xt + (size_t)col * ldm), uniform_rsrc(Xn + (size_t)col * ldm), xbase};
-            apply_x4<B, XPipe<B, S>>(Vs, X[0], W[0], xp);
-          } else {
-            apply_x4<B>(Vs, X[0], W[0]);
-          }
+        if (pipe) {
+          S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
+          const XPipe<B, S> xp{uniform_rsrc(Xt + (size_t)col * ldm), uniform_rsrc(Xn + (size_t)col * ldm),
+                               (unsigned)((((size_t)(t & 15)) * ldm + 2 * ((t & 63) >> 4)) * sizeof(S))};
+          apply_x4<B, XPipe<B, S>>(Vs, X, W, xp);
         } else {
-          if (pipe) {
-            S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
-            XPipeN<B, S, NC> xp;
-            for (int c = 0; c < NC; ++c) {
-              xp.out[c] = uniform_rsrc(Xt + (size_t)(col + 16 * c) * ldm);
-              xp.in[c] = uniform_rsrc(Xn + (size_t)(col + 16 * c) * ldm);
-            }
-            xp.base = xbase;
-            chain_x4<B, NC>(Vs, X, W, xp);
-          } else {
-            chain_x4<B, NC>(Vs, X, W, NoPost());
-          }
+          apply_x4<B>(Vs, X, W);
         }
       }
       if (g + 1 == NG) xin = pipe;
@@ -968,9 +880,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       WMARK(6);
       if (FLOW_PF) {
 #pragma unroll
-        for (int c = 0; c < NC; ++c)
-#pragma unroll
-          for (int r = 0; r < G::NRI; ++r) H[c][r] = Hn[c][r];
+        for (int r = 0; r < G::NRI; ++r) H[r] = Hn[r];
       }
       buf ^= 1;
     }
@@ -978,8 +888,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     };
     if (!groups()) return;
 #ifndef TQR_DIAG_NOSTRIP
-    if (active && !xin)
-      for (int c = 0; c < NC; ++c) store_strip_pair<B, S>(X[c], Xt, ldm, col + 16 * c);
+    if (active && !xin) store_strip_pair<B, S>(X, Xt, ldm, col);
 #endif
     pending = tc(i);
     FST(4);
@@ -1006,7 +915,7 @@ constexpr int flow_lds_doubles() {
 }
 
 template <int B, typename S>
-__global__ __launch_bounds__(flow_nt<S>(), 1) void k_flow(FlowArgs a) {
+__global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
   extern __shared__ __align__(16) double lds[];
   int* s_task = reinterpret_cast<int*>(lds + flow_lds_doubles<B, S>());
   int* s_flag = s_task + 1;

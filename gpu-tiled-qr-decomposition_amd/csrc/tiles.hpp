@@ -383,121 +383,6 @@ __device__ __forceinline__ void apply_x4(const double* __restrict__ Vs, double (
   post.fin(X);
 }
 
-// NC column groups per wave (the chain engine at one wave per SIMD: NC = 2, 32 columns): the
-// same two phases as apply_zw<B, true, Hook, true, true> / apply_x4, every LDS operand read once
-// and used for all NC groups (half the LDS read bytes per MFMA at NC = 2) and NC times as many
-// independent accumulation chains per operand.
-template <int B, int NC, typename Hook>
-__device__ __forceinline__ void chain_zw(const double* __restrict__ Vs, const double* __restrict__ Ts,
-                                         const double (&X)[NC][Geo<B>::NKS], double (&H)[NC][Geo<B>::NRI],
-                                         double (&W)[NC][Geo<B>::NRI], const Hook& hook) {
-  using g = Geo<B>;
-  constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP;
-  const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
-  double Z[NC][NRI];
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-#pragma unroll
-    for (int r = 0; r < NRI; ++r) Z[c][r] = H[c][r];
-  const unsigned vz = lds_base(Vs + x * VP + y * NRI);  // (see apply_zw)
-  auto ldz = [&](double (&a)[NRI], int ks) {
-#pragma unroll
-    for (int h = 0; h < NRI / 2; ++h) {
-      const d2v_t t = lds_rd2(vz + (unsigned)((4 * ks * VP + 2 * h) * sizeof(double)));
-      a[2 * h] = t.x;
-      a[2 * h + 1] = t.y;
-    }
-  };
-  double ac[NRI], an[NRI];
-  ldz(ac, 0);
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("" ::: "memory");
-    if ((ks & 1) == 0) hook.step(ks / 2);
-    if (ks + 1 < NKS) ldz(an, ks + 1);
-#pragma unroll
-    for (int r = 0; r < NRI; ++r)
-#pragma unroll
-      for (int c = 0; c < NC; ++c) Z[c][r] = mfma4(ac[r], X[c][ks], Z[c][r]);
-#pragma unroll
-    for (int r = 0; r < NRI; ++r) ac[r] = an[r];
-  }
-  for (int m = NKS / 2; m < Hook::STEPS; ++m) hook.step(m);
-  hook.mid();
-  // W = -T^T Z from the packed T image (see apply_zw, TPACK)
-  auto ldt = [&](double (&a)[NRI], int kb) {
-    const double2* tr = reinterpret_cast<const double2*>(Ts + ((kb * 4 + x) * 4 + y) * NRI);
-#pragma unroll
-    for (int h = 0; h < NRI / 2; ++h) {
-      const double2 v = tr[h];
-      a[2 * h] = v.x;
-      a[2 * h + 1] = v.y;
-    }
-  };
-  double tc[NRI], tn[NRI];
-  ldt(tc, 0);
-#pragma unroll
-  for (int kb = 0; kb < NRI; ++kb) {
-    __builtin_amdgcn_sched_barrier(0);
-    if (kb + 1 < NRI) ldt(tn, kb + 1);
-#pragma unroll
-    for (int wi = kb; wi < NRI; ++wi)
-#pragma unroll
-      for (int c = 0; c < NC; ++c) W[c][wi] = mfma4(tc[wi], Z[c][kb], kb == 0 ? 0.0 : W[c][wi]);
-#pragma unroll
-    for (int r = 0; r < NRI; ++r) tc[r] = tn[r];
-  }
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-#pragma unroll
-    for (int r = 0; r < NRI; ++r) H[c][r] += W[c][r];
-}
-template <int B, int NC, typename Post>
-__device__ __forceinline__ void chain_x4(const double* __restrict__ Vs, double (&X)[NC][Geo<B>::NKS],
-                                         const double (&W)[NC][Geo<B>::NRI], const Post& post) {
-  using g = Geo<B>;
-  constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP, NH = NRI / 2;
-  static_assert(NKS % 4 == 0 && NH % 2 == 0, "chain_x4 blocks");
-  const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
-  const unsigned vx = lds_base(Vs + y * VP + x * NRI);
-  auto ldh = [&](double (&a)[4][NH], int kb, int half) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int q = 0; q < NH / 2; ++q) {
-        const d2v_t t = lds_rd2(vx + (unsigned)((4 * (kb + u) * VP + half * NH + 2 * q) * sizeof(double)));
-        a[u][2 * q] = t.x;
-        a[u][2 * q + 1] = t.y;
-      }
-  };
-  double oc[4][NH], on[4][NH];
-  ldh(oc, 0, 0);
-#pragma unroll
-  for (int kb = 0; kb < NKS; kb += 4) {
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("" ::: "memory");
-      if (half == 0) ldh(on, kb, 1);
-      else if (kb + 4 < NKS) ldh(on, kb + 4, 0);
-#pragma unroll
-      for (int q = 0; q < NH; ++q)
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int c = 0; c < NC; ++c) X[c][kb + u] = mfma4(oc[u][q], W[c][half * NH + q], X[c][kb + u]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int q = 0; q < NH; ++q) oc[u][q] = on[u][q];
-    }
-    post.at(kb / 2, X);
-    post.at(kb / 2 + 1, X);
-  }
-  post.fin(X);
-}
-
 template <int B, bool HEAD, bool PF = true, bool TPACK = false>
 __device__ __forceinline__ void apply_group(const double* __restrict__ Vs, const double* __restrict__ Ts,
                                             double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI], int ks0) {
