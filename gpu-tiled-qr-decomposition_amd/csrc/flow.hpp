@@ -666,30 +666,6 @@ struct XPipe {
   }
   __device__ __forceinline__ void fin(double (&X)[Geo<B>::NKS]) const { xfer(Geo<B>::NKS / 2 - 1, X); }
 };
-#ifdef TQR_HEAD_IN_P2
-// Head-row I/O inside phase 2 (apply_x4 post hook, wrapping the strip hand-over): the group's
-// final head rows H are stored after the first k-step pair, the next group's Hn loaded after the
-// third — branch-free inside the MFMA stream: the store goes out through two resources of which
-// exactly one is live (write-back inside a segment, write-through in its last element), and
-// a load with nothing to fetch reads an empty resource (zeros, never used).
-template <int B, typename S, typename Inner>
-struct HeadPost {
-  Inner inner;
-  const double (&H)[Geo<B>::NRI];
-  double (&Hn)[Geo<B>::NRI];
-  __amdgpu_buffer_rsrc_t wb, wt, ld;
-  unsigned so, lo;
-  __device__ __forceinline__ void at(int h, double (&X)[Geo<B>::NKS]) const {
-    inner.at(h, X);
-    if (h == 1) {
-      store_head_buf<B, S, 0>(H, wb, so);
-      store_head_buf<B, S, 16>(H, wt, so);
-    }
-    if (h == 3) load_head_buf<B, S, 16>(Hn, ld, lo);
-  }
-  __device__ __forceinline__ void fin(double (&X)[Geo<B>::NKS]) const { inner.fin(X); }
-};
-#endif
 
 // Elements: UNMQR(k,j) (segment 0 only, GE-type, the strip of tile (k,j) is X) and TSMQR(i,j,k)
 // for i in [i0,i1) (TS-type: X = strip of tile (i,j), head rows = strip of tile (k,j), group by
@@ -822,11 +798,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         // first group after a streamed hand-over (the previous element's strip stores, Tc)
         const bool full = !has_next || (xin && g == 1);
         WMARK(2);
-#ifdef TQR_HEAD_IN_P2
-        constexpr int NH = 3 * G::NRI;  // head stores (two resources) + next head loads
-#else
         constexpr int NH = FLOW_PF ? 2 * G::NRI : G::NRI;  // head stores + next head loads
-#endif
         if (!(g == 0 ? sync_point_first<NX, PT>(ok, sflag, par, active)
                      : full ? sync_point<true, false, PT>(ok, sflag, par) : sync_point_cnt<NH, PT>(ok, sflag, par)))
           return false;
@@ -879,7 +851,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
 #endif
       FST(15);
       WMARK(4);
-#if !defined(TQR_DIAG_NOHEAD) && !defined(TQR_HEAD_IN_P2)
+#ifndef TQR_DIAG_NOHEAD
       if (active) {
         // head rows stay with this workgroup inside the segment (plain write-back stores); the
         // segment's last element hands them to the next segment group by group: write-through
@@ -894,21 +866,6 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       WMARK(5);
       phase_prio(true);
       if (active) {
-#ifdef TQR_HEAD_IN_P2
-        const __amdgpu_buffer_rsrc_t hnone = head_rsrc(At, false);
-        const __amdgpu_buffer_rsrc_t hld = g + 1 < NG ? hrs : hnone;
-        const unsigned hso = hoff + g * IB * sizeof(S), hlo = hoff + (g + 1) * IB * sizeof(S);
-        if (pipe) {
-          S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
-          const XPipe<B, S> xp{uniform_rsrc(Xt + (size_t)col * ldm), uniform_rsrc(Xn + (size_t)col * ldm),
-                               (unsigned)((((size_t)(t & 15)) * ldm + 2 * ((t & 63) >> 4)) * sizeof(S))};
-          const HeadPost<B, S, XPipe<B, S>> hp{xp, H, Hn, has_next ? hrs : hnone, has_next ? hnone : hrs, hld, hso, hlo};
-          apply_x4<B, HeadPost<B, S, XPipe<B, S>>>(Vs, X, W, hp);
-        } else {
-          const HeadPost<B, S, NoPost> hp{NoPost(), H, Hn, has_next ? hrs : hnone, has_next ? hnone : hrs, hld, hso, hlo};
-          apply_x4<B, HeadPost<B, S, NoPost>>(Vs, X, W, hp);
-        }
-#else
         if (pipe) {
           S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
           const XPipe<B, S> xp{uniform_rsrc(Xt + (size_t)col * ldm), uniform_rsrc(Xn + (size_t)col * ldm),
@@ -917,7 +874,6 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         } else {
           apply_x4<B>(Vs, X, W);
         }
-#endif
       }
       if (g + 1 == NG) xin = pipe;
       FST(13);
