@@ -152,6 +152,24 @@ def check_output(A0, A, m, n):
     return rel
 
 
+def check_owned_columns(A0, A, m, n, b, rank, world):
+    """The same check for one rank of a multi-GPU factorisation: every column of R lives in its
+    tile column, and a tile column is finished by its owner (panel and all its updates), so each
+    rank checks the columns it owns (tile columns j = rank mod world) on its own device."""
+    import torch
+    q = n // b
+    cols = torch.arange(n, device=A.device).view(q, b)[rank::world].reshape(-1)
+    Ao = A[cols].double()  # (n, m) storage: row c = matrix column c
+    keep = torch.arange(m, device=A.device)[None, :] <= cols[:, None]  # R: rows r <= c
+    nr = torch.linalg.vector_norm(Ao * keep, dim=1)
+    na = torch.linalg.vector_norm(A0[cols].double(), dim=1)
+    rel = ((na - nr).abs() / na.clamp_min(1e-300)).max().item()
+    tol = 1e-10 if A.dtype == torch.float64 else 1e-4
+    if not rel <= tol:
+        raise RuntimeError(f"bench: rank {rank}: factorisation check failed (column-norm error {rel:.3e} > {tol})")
+    return rel
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,12 +246,12 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     plan.status(stream)
-    ok_rel = check_output(A0, A, m, n) if world == 1 else None
+    ok_rel = check_output(A0, A, m, n) if world == 1 else check_owned_columns(A0, A, m, n, b, rank, world)
     dist_info = None
     if dist:
         # per rank: engine status (raised above if not ok), forwarded bytes, and with a stamps build
         # (TQR_LIB=libtqr_fst.so) the share of workgroup time the forward tasks took
-        mine = {"rank": rank, "status": "ok", "fwd_bytes": plan.fwd_bytes()}
+        mine = {"rank": rank, "status": "ok", "fwd_bytes": plan.fwd_bytes(), "column_norm_rel_err": ok_rel}
         L = tqr.lib()
         if hasattr(L, "tqr_debug_flow_stamps"):
             import ctypes

@@ -808,10 +808,19 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
         hipMalloc(&pl->d_wk, sizeof(double*) * pl->kmax) != hipSuccess) {
       tqr_plan_destroy(pl); return TQR_ENOMEM;
     }
-    // one workspace per step k: V then T images of tiles (k..p-1, k), every group
+    // one workspace per step k: V then T images of tiles (k..p-1, k), every group.
+    // Multi-GPU: peers' forward tasks write images of their panels into these slots over xGMI,
+    // and such writes do not pass through this device's L2 — a line of a slot left in L2 by the
+    // previous execute's reads would be served stale to this execute's chains. The slots are
+    // therefore uncached (like the member flags); TQR_DIST_WK_CACHED=1 keeps them cached (the
+    // one-GPU rehearsal's A/B of that cost only).
+    const bool wk_uc = world > 1 && !(getenv("TQR_DIST_WK_CACHED") && atoi(getenv("TQR_DIST_WK_CACHED")) == 1);
     for (int k = 0; k < pl->kmax; ++k) {
       double* w = nullptr;
-      if (hipMalloc(&w, wk_bytes(b, pl->p - k, dtype)) != hipSuccess) { tqr_plan_destroy(pl); return TQR_ENOMEM; }
+      const size_t wb = wk_bytes(b, pl->p - k, dtype);
+      if ((wk_uc ? hipExtMallocWithFlags((void**)&w, wb, hipDeviceMallocUncached) : hipMalloc(&w, wb)) != hipSuccess) {
+        tqr_plan_destroy(pl); return TQR_ENOMEM;
+      }
       pl->wk.push_back(w);
     }
     if (hipMemcpy(pl->d_wk, pl->wk.data(), sizeof(double*) * pl->kmax, hipMemcpyHostToDevice) != hipSuccess) {
