@@ -261,7 +261,7 @@ def main():
             stv = (ctypes.c_ulonglong * (nc * grid.value))()
             if L.tqr_debug_flow_stamps(stv, grid.value) == 0:
                 tot = sum(stv)
-                fwd = sum(stv[w * nc + 23] for w in range(grid.value))
+                fwd = sum(stv[w * nc + 23] for w in range(grid.value))  # panels' image forwarding
                 mine["fwd_share_of_wg_time"] = round(fwd / tot, 4) if tot else None
                 mine["fwd_ms_per_wg"] = round(fwd / grid.value / 1e5, 3)  # s_memrealtime at 100 MHz
         ranks = [None] * world

@@ -508,10 +508,10 @@ static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp) {
   }
 }
 // Multi-GPU: keep this rank's share of the global (topological) order — panel tasks of the tile
-// columns it owns (column k on rank k % world) each followed by the forward task of that panel
-// member, and the chain tasks of its own tile columns. Every rank's list is the global order
-// restricted (FWD(i,k) sits right after QRD(i,k)), so the earliest unfinished task of the whole
-// job can always progress: the multi-rank engine is deadlock-free like the single-GPU one.
+// columns it owns (column k on rank k % world; each forwards its images to the peers itself) and
+// the chain tasks of its own tile columns. Every rank's list is the global order restricted, so
+// the earliest unfinished task of the whole job can always progress: the multi-rank engine is
+// deadlock-free like the single-GPU one.
 static void partition_flow_plan(FlowPlan& fp, int rank, int world) {
   std::vector<Item> mine;
   for (const Item& it : fp.items) {
@@ -520,7 +520,6 @@ static void partition_flow_plan(FlowPlan& fp, int rank, int world) {
       if (it.m % world == rank) mine.push_back(it);
     } else if (it.k % world == rank) {  // QRS(k,k) / QRD(l,k): tile column k
       mine.push_back(it);
-      mine.push_back(Item{T_FWD, it.l, it.k, it.k});
     }
   }
   fp.items.swap(mine);
@@ -996,9 +995,10 @@ int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, in
   build_flow_plan(M, N, b, seglen, fp);
   if (world > 1) partition_flow_plan(fp, rank, world);
   if (ntasks) *ntasks = (int)fp.items.size();
-  if (nfwd) {
+  if (nfwd) {  // panel members that forward their images (the panel tasks, when world > 1)
     int c = 0;
-    for (auto& it : fp.items) c += (it.ts & 0xff) == T_FWD;
+    if (world > 1)
+      for (auto& it : fp.items) c += (it.ts & 0xff) != T_CHAIN;
     *nfwd = c;
   }
   return TQR_OK;

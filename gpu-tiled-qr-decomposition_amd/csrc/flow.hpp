@@ -33,7 +33,6 @@
 namespace tqr {
 
 constexpr int T_CHAIN = 4;
-constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel member to every peer
 
 // Diagnostic build only (make flowstamps): per-workgroup s_memrealtime sums by activity.
 // Every FST(c) charges the time since the previous stamp to category c (LDS-resident sums,
@@ -48,8 +47,8 @@ constexpr int T_FWD = 5;  // multi-GPU: forward the V/T images of one panel memb
 // start (lookahead column j = k+1 / other columns), 20 chain Rc waits inside a lookahead-column
 // element (0 is then the same for other columns), 21 / 22 chain drain of the wave's own memory
 // operations before the group's polls, groups > 0 / group 0 (stamps build only; at group 0 this
-// includes the element's strip loads, which the real kernel overlaps with phase 1), 23 forward
-// tasks (multi-GPU: panel images copied to the peers, including their waits for the panel).
+// includes the element's strip loads, which the real kernel overlaps with phase 1), 23 panel
+// forwarding (multi-GPU: issuing the group's image copies to the peers, setting their flags).
 constexpr int FST_N = 24;
 constexpr int WSL = 8;  // per-wave stamp slots
 #ifdef TQR_FLOW_STAMPS
@@ -440,6 +439,27 @@ template <int B>
 __device__ __noinline__ void write_images32(const double* Vs, const double* Ts, __amdgpu_buffer_rsrc_t rv,
                                             __amdgpu_buffer_rsrc_t rt);
 
+// Multi-GPU: the panel task itself copies each group's V and T images from its workspace slot
+// into every peer's (16-B system-scope stores over xGMI), right after the group's Rc publish;
+// its next publish (Rt, after the in-tile trailing update) drains them, then thread 0 releases at
+// system scope and sets the peers' member flags Rf[k][i][g]. (Round 2 had a separate forward
+// task per member, dequeued right behind it: it held a workgroup while waiting for the member's
+// groups — 5.4 % of workgroup time in the 2-rank rehearsal, 682 vs 667 ms for this form.)
+template <int B, typename S>
+__device__ __forceinline__ void fwd_images(const FlowArgs& a, int k, size_t vo, size_t to) {
+  const __amdgpu_buffer_rsrc_t vsrc = uniform_rsrc(a.Wk[k] + vo), tsrc = uniform_rsrc(a.Wk[k] + to);
+  for (int r = 0; r < a.world; ++r) {
+    if (r == a.rank) continue;
+    double* pw = a.peers[r].Wk[k];
+    const __amdgpu_buffer_rsrc_t vdst = uniform_rsrc(pw + vo), tdst = uniform_rsrc(pw + to);
+#pragma unroll 4
+    for (int c = threadIdx.x; c < Img<B, S>::V / 2; c += blockDim.x)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(vsrc, 16 * c, 0, 16), vdst, 16 * c, 0, 17);
+    for (int c = threadIdx.x; c < Img<B, S>::T / 2; c += blockDim.x)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(tsrc, 16 * c, 0, 16), tdst, 16 * c, 0, 17);
+  }
+}
+
 // ---- panel tasks ---------------------------------------------------------------------------
 template <int B, typename S>
 __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* lds, int* sflag) {
@@ -472,7 +492,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
   double X[G::NKS];
   double H[G::NRI];
   for (int g = 0; g < NG; ++g) {
-    const int c0 = g * IB, ks0 = c0 / 4;
+    const int c0 = g * IB;
     if (!qrs) {  // R_kk rows of group g as left by the previous chain member
       FST(10);
       const bool ok = t == FLOW_PT ? spin_ge(&a.Rr[(size_t)k * NG + g], pos, a.err) : true;
@@ -555,6 +575,9 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
     wg_publish(&a.Rc[(size_t)k * NG + g], 1);
     FST(10);
+    // multi-GPU: the images to every peer (drained by the Rt publish below, flags after it)
+    if (a.dist) fwd_images<B, S>(a, k, flow_vw_off<B, S>(a.p, qrs ? k : l, k, g), flow_tw_off<B, S>(a.p, qrs ? k : l, k, g));
+    FST(23);
     if (!qrs) {  // R_kk head rows right of the group as left by the previous member's trailing
       const bool ok = t == FLOW_PT ? spin_ge(&a.Rt[(size_t)k * NG + g], pos, a.err) : true;
       if (!wg_verdict(ok, sflag)) return;
@@ -591,47 +614,14 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     }
     wg_publish(&a.Rt[(size_t)k * NG + g], 1);
     FST(12);
-  }
-}
-
-// ---- forward tasks (multi-GPU) -------------------------------------------------------------
-// FWD(i,k) on the owner of panel k: group by group, once member i finished group g here, copy the
-// V and T images of (i,k,g) into every peer's workspace with system-scope (sc0 sc1) 16-B stores
-// over xGMI, drain, release at system scope, and set each peer's flag Rf[k][i][g]. Peers' chains
-// then LDS-DMA the images from their own HBM exactly as the owner's chains do. Per-member flags
-// (not counters) let the forwards of different members run concurrently on different
-// workgroups: a panel's images leave as fast as they are produced.
-template <int B, typename S>
-__device__ __noinline__ void flow_fwd(const FlowArgs& a, int i, int k, int* sflag) {
-  using G = Geo<B>;
-  constexpr int NG = G::NG;
-  const int t = threadIdx.x, pos = i - k;
-  for (int g = 0; g < NG; ++g) {
-    bool ok = true;
-    if (t == FLOW_PT) ok = spin_ge(&a.Rc[(size_t)k * NG + g], pos + 1, a.err);
-    if (!wg_verdict(ok, sflag)) return;
-    const size_t vo = flow_vw_off<B, S>(a.p, i, k, g), to = flow_tw_off<B, S>(a.p, i, k, g);
-    const __amdgpu_buffer_rsrc_t vsrc = uniform_rsrc(a.Wk[k] + vo), tsrc = uniform_rsrc(a.Wk[k] + to);
-    for (int r = 0; r < a.world; ++r) {
-      if (r == a.rank) continue;
-      double* pw = a.peers[r].Wk[k];
-      const __amdgpu_buffer_rsrc_t vdst = uniform_rsrc(pw + vo), tdst = uniform_rsrc(pw + to);
-      for (int c = t; c < Img<B, S>::V / 2; c += FLOW_NT)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(vsrc, 16 * c, 0, 16), vdst, 16 * c, 0, 17);
-      for (int c = t; c < Img<B, S>::T / 2; c += FLOW_NT)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(tsrc, 16 * c, 0, 16), tdst, 16 * c, 0, 17);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
+    if (a.dist && t == 0) {  // every wave's peer stores drained (the Rt publish): release, flags
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
-      const size_t fo = ((size_t)k * a.p + i) * NG + g;
+      const size_t fo = ((size_t)k * a.p + (qrs ? k : l)) * NG + g;
       for (int r = 0; r < a.world; ++r)
         if (r != a.rank) __hip_atomic_store(&a.peers[r].Rf[fo], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __syncthreads();
+    FST(23);
   }
-  FST(23);
 }
 
 // ---- chain tasks ---------------------------------------------------------------------------
@@ -954,8 +944,6 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
       else
         flow_chain32<B>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                         s_flag);
-    } else if (type == T_FWD) {
-      flow_fwd<B, S>(a, it.l, it.k, s_flag);
     } else {
       flow_panel<B, S>(a, type, it.l, it.k, lds, s_flag);
     }

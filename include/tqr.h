@@ -126,7 +126,8 @@ int tqr_dist_owner(const tqr_plan* plan, int tile_col);
 /* bytes this rank forwards to its peers per factorisation (every owned panel member's V/T images,
  * all reflector groups, to each of the world - 1 peers); 0 for a single-GPU plan */
 long long tqr_plan_fwd_bytes(const tqr_plan* plan);
-/* host-only: this rank's task-list length and number of forward tasks */
+/* host-only: this rank's task-list length and the number of its panel members that forward
+ * their V/T images to the peers (its panel tasks when world > 1, else 0) */
 int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd);
 
 /* ---- one-shot helpers ------------------------------------------------------------------ */

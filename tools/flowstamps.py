@@ -27,7 +27,7 @@ assert L.tqr_debug_flow_stamps(st, nb) == 0
 names = ["chain Rc wait in-elem other", "panel waits", "chain head-row store", "chain phase 1 Z (+DMA)",
          "chain strip I/O+publish", "panel_factor", "dequeue/dispatch/exit", "chain drain+barrier",
          "chain Tc waits", "chain Ac waits", "panel I/O+images", "panel build_t", "panel trail MFMA+publish", "chain phase 2", "chain next-head load", "chain W + head update", "panel trail loads", "panel trail stores",
-         "chain Rc wait @start la-col", "chain Rc wait @start other", "chain Rc wait in-elem la-col", "chain own-memory drain @group>0", "chain own-memory drain @group0", "fwd tasks (multi-GPU)"]
+         "chain Rc wait @start la-col", "chain Rc wait @start other", "chain Rc wait in-elem la-col", "chain own-memory drain @group>0", "chain own-memory drain @group0", "panel fwd to peers (multi-GPU)"]
 tot = [sum(st[w * NC + c] for w in range(nb)) for c in range(NC)]
 allt = sum(tot)
 print(f"{m}x{n} b={b}: wall {ms:.1f} ms; {nb} workgroups; sum of stamps {allt / nb / 1e5:.1f} ms per WG")

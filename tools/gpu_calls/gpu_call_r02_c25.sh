@@ -1,9 +1,18 @@
+# panel-side forwarding (TQR_PANEL_FWD, no FWD tasks): dist parity on one GPU, rehearsal A/B (2 ranks x 128 CUs), stamps
 set -o pipefail
-mkdir -p gpurun_out/r02_c25
-TQR_LIB=libtqr_v5.so timeout -k 10 200 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread -k "factor_f32_b32 or factor_f32_b16" > gpurun_out/r02_c25/pytest_v5.log 2>&1; echo "v5 rc=$?"; tail -1 gpurun_out/r02_c25/pytest_v5.log
-timeout -k 10 400 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread -k "f32 or fp32 or float32" > gpurun_out/r02_c25/pytest_f32.log 2>&1 || { echo "pytest failed"; grep -E "^FAILED|passed|failed" gpurun_out/r02_c25/pytest_f32.log; exit 1; }
-tail -1 gpurun_out/r02_c25/pytest_f32.log
-timeout -k 10 200 python bench.py --no-cpu-baseline --no-host-api --steps 5 --warmup 2 --storage f32 --rows 32768 --cols 32768 > gpurun_out/r02_c25/bench_f32.json 2> gpurun_out/r02_c25/bench_f32.err || { echo bench failed; tail gpurun_out/r02_c25/bench_f32.err; exit 1; }
-python3 -c "import json;d=json.loads(open('gpurun_out/r02_c25/bench_f32.json').read());print(d['ms_per_step'], d['roofline']['frac'])"
-TQR_FST_LIB=libtqr_fst.so TQR_FST_DTYPE=f32 timeout -k 10 200 python tools/flowstamps.py 32768 > gpurun_out/r02_c25/fst.txt 2>&1 || { echo "fst failed"; tail gpurun_out/r02_c25/fst.txt; exit 1; }
-grep -E "wall|phase|store|Rc wait in-elem other|strip|drain" gpurun_out/r02_c25/fst.txt
+OUT=gpurun_out/c25; mkdir -p $OUT
+export TMPDIR=/tmp
+TQR_LIB=libtqr_pfwd.so timeout -k 10 600 python -u -m pytest tests/test_dist.py -v -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_dist_pfwd.log 2>&1 || { echo "pytest dist pfwd failed"; tail -30 $OUT/pytest_dist_pfwd.log; exit 1; }
+tail -2 $OUT/pytest_dist_pfwd.log
+n=0
+for r in 1 2; do
+for L in libtqr.so libtqr_pfwd.so; do
+n=$((n+1))
+TQR_LIB=$L TQR_BENCH_DEVICE=0 TQR_BENCH_BACKEND=gloo TQR_FLOW_GRID=128 timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 2954$n bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline > $OUT/reh_${L}_$r.json 2> $OUT/reh_${L}_$r.err || { echo "rehearsal $L failed"; tail -20 $OUT/reh_${L}_$r.err; exit 1; }
+python3 -c "import json;d=json.loads(open('$OUT/reh_${L}_$r.json').read().strip().splitlines()[-1]);print('$L', d['ms_per_step'], d['value'], [x['column_norm_rel_err'] for x in d['dist']['ranks']])"
+done
+done
+for L in libtqr_fst.so libtqr_diag_pfwd.so; do
+TQR_LIB=$L TQR_BENCH_DEVICE=0 TQR_BENCH_BACKEND=gloo TQR_FLOW_GRID=128 timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29549 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline > $OUT/reh_stamps_$L.json 2> $OUT/reh_stamps_$L.err || { echo "stamps $L failed"; tail -20 $OUT/reh_stamps_$L.err; exit 1; }
+python3 -c "import json;d=json.loads(open('$OUT/reh_stamps_$L.json').read().strip().splitlines()[-1]);print('$L', d['ms_per_step'], json.dumps(d['dist'])[:500])"
+done
