@@ -240,7 +240,8 @@ class DistTiledQR(TiledQR):
 
 
 def dist_plan_check(M, N, b, rank, world, seglen=8):
-    """Host-only: (ntasks, n_forward_tasks) of one rank's task list."""
+    """Host-only: (ntasks, n_forwarding_members) of one rank's task list (its panel tasks forward
+    their images to the peers when world > 1)."""
     nt, nf = _I(), _I()
     check(lib().tqr_dist_plan_check(M, N, b, seglen, rank, world, ctypes.byref(nt), ctypes.byref(nf)),
           "tqr_dist_plan_check")
