@@ -808,7 +808,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
       tqr_plan_destroy(pl); return TQR_ENOMEM;
     }
     // one workspace per step k: V then T images of tiles (k..p-1, k), every group.
-    // Multi-GPU: peers' forward tasks write images of their panels into these slots over xGMI,
+    // Multi-GPU: peers' panel tasks write images of their panels into these slots over xGMI,
     // and such writes do not pass through this device's L2 — a line of a slot left in L2 by the
     // previous execute's reads would be served stale to this execute's chains. The slots are
     // therefore uncached (like the member flags); TQR_DIST_WK_CACHED=1 keeps them cached (the
