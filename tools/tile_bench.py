@@ -31,9 +31,17 @@ for dt, code, name in ((np.float64, 1, "f64"), (np.float32, 0, "f32")):
             out = np.zeros((nb * b, rows * b), dt)
             ms = ctypes.c_float()
             best = None
+            rc = 0
             for rep in range(3):
                 rc = L.tqr_tile_batch(code, typ, b, nb, vp(V), b, vp(tau), vp(blk), rows * b, vp(out), rows * b,
                                       ctypes.byref(ms))
+                # a batch beyond the 32-bit offsets of tqr_tile_batch's device matrix is rejected
+                # (TQR_EINVAL, before any launch): halve it until it fits
+                while rc == -1 and rep == 0 and nb > 64:
+                    nb //= 2
+                    out = out[:nb * b]
+                    rc = L.tqr_tile_batch(code, typ, b, nb, vp(V), b, vp(tau), vp(blk), rows * b, vp(out), rows * b,
+                                          ctypes.byref(ms))
                 if rc != 0:
                     break
                 best = ms.value if best is None else min(best, ms.value)
