@@ -566,8 +566,19 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       double* vg = flow_vw<B, S>(a, qrs ? k : l, k, g);
       const __amdgpu_buffer_rsrc_t rv = uniform_rsrc(vg), rt = uniform_rsrc(tg);
       if constexpr (sizeof(S) == 8) {
-        for (int idx = t; idx < G::TPIMG / 2; idx += FLOW_NT) st_pair<double>(rt, 16 * idx, Tp[2 * idx], Tp[2 * idx + 1]);
-        for (int idx = t; idx < G::VSZ / 2; idx += FLOW_NT) st_pair<double>(rv, 16 * idx, Vs[2 * idx], Vs[2 * idx + 1]);
+        // the chain's images in the paired reflector order (tiles.hpp sigp): V image position
+        // x * NRI + r of a row holds reflector sigp(r, x); packed -T over k-blocks kb >= (wi & ~1)
+        constexpr int NRI = G::NRI;
+        auto tpk = [&](int e) -> double {
+          const int wi = e % NRI, y = (e / NRI) & 3, x = (e / (4 * NRI)) & 3, kb = e / (16 * NRI);
+          return e < G::TPK && (kb & ~1) <= wi ? -Ts[sigp(kb, x) * TP + sigp(wi, y)] : 0.0;
+        };
+        auto vim = [&](int e) -> double {
+          const int row = e / VP, pos = e % VP;
+          return pos < IB ? Vs[row * VP + G::pc(sigp(pos % NRI, pos / NRI))] : 0.0;
+        };
+        for (int idx = t; idx < G::TPIMG / 2; idx += FLOW_NT) st_pair<double>(rt, 16 * idx, tpk(2 * idx), tpk(2 * idx + 1));
+        for (int idx = t; idx < G::VSZ / 2; idx += FLOW_NT) st_pair<double>(rv, 16 * idx, vim(2 * idx), vim(2 * idx + 1));
       } else {
         write_images32<B>(Vs, Ts, rv, rt);  // the fp32 chain's operand images (chain32.hpp)
       }
@@ -677,6 +688,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   const size_t ldm = a.ldm;
   const int t = threadIdx.x, w = t >> 6;
   constexpr int PT = FLOW_CHAIN_PT;
+  constexpr int HPACK = 2;  // head rows per lane and access (16-B paired head rows, tiles.hpp sigp)
   const int col = s * FLOW_SW + 16 * w;  // this wave's 16 columns inside the tile
   const bool active = B % FLOW_SW == 0 || col < B;  // (compile-time true unless B < FLOW_SW)
   S* At = A + (size_t)j * B * ldm + (size_t)k * B;  // tile (k,j): the chain's head rows
@@ -746,8 +758,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     // element types keeps the register allocation of the hot TSMQR path clean (a separate GE
     // variant with ks0-skipping cost the TSMQR phase 2 its operand prefetch), for ~1 % extra flops.
     const __amdgpu_buffer_rsrc_t hrs = head_rsrc(At + (size_t)col * ldm, ts);  // UNMQR: empty resource, head = 0
-    const unsigned hoff = head_off<B, S>(ldm, 0);
-    if (FLOW_PF && active) load_head_buf<B, S, 16>(H, hrs, hoff);
+    const unsigned hoff = head_off_pair<B>(ldm, 0);
+    if (FLOW_PF && active) load_head_pair<B, 16>(H, hrs, hoff);
     FST(4);
     const int inext = (i == k) ? i0 : i + 1;
     const bool has_next = inext < i1;
@@ -783,12 +795,12 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         }
         FST(j == k + 1 ? 20 : 0);  // Rc wait inside an element (lookahead column / other)
         // group 0: the strip / head loads of this element may still be in flight
-        constexpr int NX = G::NKS / 2 + (FLOW_PF ? G::NRI : 0);
+        constexpr int NX = G::NKS / 2 + (FLOW_PF ? G::NRI / HPACK : 0);
         // full drain where a publish follows: the segment's last element (head rows, Ac) and the
         // first group after a streamed hand-over (the previous element's strip stores, Tc)
         const bool full = !has_next || (xin && g == 1);
         WMARK(2);
-        constexpr int NH = FLOW_PF ? 2 * G::NRI : G::NRI;  // head stores + next head loads
+        constexpr int NH = (FLOW_PF ? 2 * G::NRI : G::NRI) / HPACK;  // head stores + next head loads
         if (!(g == 0 ? sync_point_first<NX, PT>(ok, sflag, par, active)
                      : full ? sync_point<true, false, PT>(ok, sflag, par) : sync_point_cnt<NH, PT>(ok, sflag, par)))
           return false;
@@ -817,7 +829,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         if (g + 2 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
       }
       FST(7);
-      if (!FLOW_PF && active) load_head_buf<B, S, 16>(H, hrs, hoff + g * IB * sizeof(S));  // 2 waves/SIMD
+      if (!FLOW_PF && active) load_head_pair<B, 16>(H, hrs, hoff + g * IB * sizeof(S));
       const double* Vs = lds + buf * BUF;
       const double* Ts = Vs + G::VIMG;
       // the other buffer is free (every wave passed this sync point): next DMA rides phase 1
@@ -831,11 +843,11 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       d.t = timg(k, 0);
 #endif
 #ifdef TQR_DIAG_NODMA  // what-if: no staging at all
-      if (active) apply_zw<B, true, NoHook, FLOW_PF, true>(Vs, Ts, X, H, W, 0);
+      if (active) apply_zw<B, true, NoHook, FLOW_PF, true, HPACK == 2>(Vs, Ts, X, H, W, 0);
 #else
       phase_prio(false);
       WMARK(3);
-      if (active) apply_zw<B, true, DmaJob<B>, FLOW_PF, true>(Vs, Ts, X, H, W, 0, d);
+      if (active) apply_zw<B, true, DmaJob<B>, FLOW_PF, true, HPACK == 2>(Vs, Ts, X, H, W, 0, d);
       else
         for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
 #endif
@@ -846,10 +858,10 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         // head rows stay with this workgroup inside the segment (plain write-back stores); the
         // segment's last element hands them to the next segment group by group: write-through
         // stores, drained, then Ac[k][j][s][g]++ (one group later, after the next drain)
-        if (has_next) store_head_buf<B, S, 0>(H, hrs, hoff + g * IB * sizeof(S));
-        else store_head_buf<B, S, 16>(H, hrs, hoff + g * IB * sizeof(S));
+        if (has_next) store_head_pair<B, 0>(H, hrs, hoff + g * IB * sizeof(S));
+        else store_head_pair<B, 16>(H, hrs, hoff + g * IB * sizeof(S));
         FST(2);
-        if (FLOW_PF && g + 1 < NG) load_head_buf<B, S, 16>(Hn, hrs, hoff + (g + 1) * IB * sizeof(S));
+        if (FLOW_PF && g + 1 < NG) load_head_pair<B, 16>(Hn, hrs, hoff + (g + 1) * IB * sizeof(S));
       }
 #endif
       FST(14);

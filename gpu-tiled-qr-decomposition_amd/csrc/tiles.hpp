@@ -186,7 +186,13 @@ struct NoHook {
 // the other wave hides the latency and the registers are better spent elsewhere)
 // TPACK: Ts is the packed image of pack_t (W = -T^T Z as NRI batches of independent MFMAs with
 // 16-B operand reads one batch ahead) instead of the row-major T (one 8-B read per MFMA).
-template <int B, bool HEAD, typename Hook = NoHook, bool PF = true, bool TPACK = false>
+// Paired reflector order of the fp64 chain's images (PAIRH): MFMA block r = 2h + e, lane row x
+// <-> reflector 8h + 2x + e of the group, so a lane's head registers H[2h], H[2h+1] are two
+// consecutive head rows (one 16-B access, as the strips). The relabelling is a permutation of the
+// group's reflectors: T becomes block-upper-triangular at 8-reflector granularity, so W = -T^T Z
+// needs the k-blocks kb >= (wi & ~1) instead of kb >= wi (40 instead of 36 MFMAs per group).
+__device__ __forceinline__ constexpr int sigp(int r, int x) { return 8 * (r >> 1) + 2 * x + (r & 1); }
+template <int B, bool HEAD, typename Hook = NoHook, bool PF = true, bool TPACK = false, bool PAIRH = false>
 __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const double* __restrict__ Ts,
                                          const double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI],
                                          double (&W)[Geo<B>::NRI], int ks0, const Hook& hook = Hook()) {
@@ -253,7 +259,7 @@ __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const do
       __builtin_amdgcn_sched_barrier(0);
       if (kb + 1 < NRI) ldt(tn, kb + 1);
 #pragma unroll
-      for (int wi = kb; wi < NRI; ++wi) W[wi] = mfma4(tc[wi], Z[kb], kb == 0 ? 0.0 : W[wi]);
+      for (int wi = PAIRH ? (kb & ~1) : kb; wi < NRI; ++wi) W[wi] = mfma4(tc[wi], Z[kb], kb == 0 ? 0.0 : W[wi]);
 #pragma unroll
       for (int r = 0; r < NRI; ++r) tc[r] = tn[r];
     }
@@ -526,6 +532,32 @@ __device__ __forceinline__ void store_head_buf(const double (&H)[Geo<B>::NRI], _
     } else {
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint((float)H[r]), rs, base, 4 * r * 4, AUX);
     }
+  }
+}
+// Head rows of one group in the paired order (fp64 chain, PAIRH): H[2h + e] at lane x <-> row
+// r0 + 8h + 2x + e, column 4blk + y; base = head_off_pair (16-B aligned), 8 rows per access.
+template <int B>
+__device__ __forceinline__ unsigned head_off_pair(size_t ldm, int r0) {
+  const int lane = threadIdx.x & 63, x = lane >> 4, c = lane & 15;
+  return (unsigned)(((size_t)c * ldm + r0 + 2 * x) * sizeof(double));
+}
+template <int B, int AUX>
+__device__ __forceinline__ void load_head_pair(double (&H)[Geo<B>::NRI], __amdgpu_buffer_rsrc_t rs, unsigned base) {
+#pragma unroll
+  for (int h = 0; h < Geo<B>::NRI / 2; ++h) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 8 * h * 8, AUX);
+    H[2 * h] = __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
+    H[2 * h + 1] = __longlong_as_double((long long)(((unsigned long long)v[3] << 32) | v[2]));
+  }
+}
+template <int B, int AUX>
+__device__ __forceinline__ void store_head_pair(const double (&H)[Geo<B>::NRI], __amdgpu_buffer_rsrc_t rs, unsigned base) {
+#pragma unroll
+  for (int h = 0; h < Geo<B>::NRI / 2; ++h) {
+    const unsigned long long a = (unsigned long long)__double_as_longlong(H[2 * h]);
+    const unsigned long long b = (unsigned long long)__double_as_longlong(H[2 * h + 1]);
+    __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, base, 8 * h * 8, AUX);
   }
 }
 // Natural-order strip through a buffer resource (the panel's in-tile trailing update):
