@@ -1,6 +1,10 @@
+# segment length sweep with paired head rows (TQR_SEGLEN; default 8)
 set -o pipefail
-mkdir -p gpurun_out/r02_c31
-timeout -k 10 200 python bench.py --no-cpu-baseline --no-host-api > gpurun_out/r02_c31/bench.json 2> gpurun_out/r02_c31/bench.err || { echo bench failed; tail gpurun_out/r02_c31/bench.err; exit 1; }
-python3 -c "import json;d=json.loads(open('gpurun_out/r02_c31/bench.json').read());print('f64', d['ms_per_step'], d['roofline']['frac'], d.get('status'))"
-TQR_FST_LIB=libtqr_fst.so timeout -k 10 200 python tools/flowstamps.py 16384 > gpurun_out/r02_c31/fst.txt 2>&1 || { echo "fst failed"; tail gpurun_out/r02_c31/fst.txt; exit 1; }
-grep -E "wall|phase|drain|barrier|wave" gpurun_out/r02_c31/fst.txt
+OUT=gpurun_out/c31; mkdir -p $OUT
+export TMPDIR=/tmp
+for r in 1 2; do
+for S in 8 6 10 12 16; do
+  TQR_SEGLEN=$S timeout -k 10 120 python bench.py --no-cpu-baseline --no-host-api --steps 10 --warmup 2 > $OUT/bench_s${S}_$r.json 2> $OUT/bench_s${S}_$r.err || { echo "bench $S failed"; tail -20 $OUT/bench_s${S}_$r.err; exit 1; }
+  echo "seglen $S $(python3 -c "import json,sys; d=json.load(open('$OUT/bench_s${S}_$r.json')); print(d['ms_per_step'], d['value'], d['roofline']['frac'])")"
+done
+done
