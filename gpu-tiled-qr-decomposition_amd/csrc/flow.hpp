@@ -104,7 +104,14 @@ extern __device__ unsigned long long g_wst[];
 constexpr int FLOW_NT = 512;
 constexpr int FLOW_NW = FLOW_NT / 64;      // waves
 constexpr int FLOW_SW = 16 * FLOW_NW;      // strip width (columns) of a chain task
-constexpr bool FLOW_PF = true;  // software-pipelined operand reads (also at 2 waves/SIMD)
+constexpr bool FLOW_PF = true;
+// cache policy of the chain's in-segment head-row traffic (buffer aux bits; 16 = sc1, 2 = nt)
+#ifndef TQR_HEAD_ST_AUX
+#define TQR_HEAD_ST_AUX 0
+#endif
+#ifndef TQR_HEAD_LD_AUX
+#define TQR_HEAD_LD_AUX 18  // sc1 | nt: 129.86 vs 130.03-130.14 ms (2 A/B rounds; nt stores: 130.2, slower)
+#endif  // software-pipelined operand reads (also at 2 waves/SIMD)
 // The thread that polls a task's dependency counters, keeps the Rc view and writes the sync-point
 // verdicts (publishes stay with thread 0).
 #ifndef TQR_POLL_T
@@ -858,10 +865,10 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         // head rows stay with this workgroup inside the segment (plain write-back stores); the
         // segment's last element hands them to the next segment group by group: write-through
         // stores, drained, then Ac[k][j][s][g]++ (one group later, after the next drain)
-        if (has_next) store_head_pair<B, 0>(H, hrs, hoff + g * IB * sizeof(S));
+        if (has_next) store_head_pair<B, TQR_HEAD_ST_AUX>(H, hrs, hoff + g * IB * sizeof(S));
         else store_head_pair<B, 16>(H, hrs, hoff + g * IB * sizeof(S));
         FST(2);
-        if (FLOW_PF && g + 1 < NG) load_head_pair<B, 16>(Hn, hrs, hoff + (g + 1) * IB * sizeof(S));
+        if (FLOW_PF && g + 1 < NG) load_head_pair<B, TQR_HEAD_LD_AUX>(Hn, hrs, hoff + (g + 1) * IB * sizeof(S));
       }
 #endif
       FST(14);

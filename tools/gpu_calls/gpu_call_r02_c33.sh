@@ -1,4 +1,12 @@
+# chain head-row cache policy: in-segment stores nt (aux 2), loads sc1|nt (aux 18), both; A/B x2
 set -o pipefail
-mkdir -p gpurun_out/r02_c33
-timeout -k 10 120 tools/ubench/mfma_f64 > gpurun_out/r02_c33/ubench_mfma.txt 2>&1
-cat gpurun_out/r02_c33/ubench_mfma.txt | grep -E "4x4x4|device"
+OUT=gpurun_out/c33; mkdir -p $OUT
+export TMPDIR=/tmp
+TQR_LIB=libtqr_hboth.so timeout -k 10 300 python -u -m pytest tests/test_gpu_factor.py -q -x -m gpu --timeout 120 --timeout-method thread -k "vs_oracle or vs_reference" > $OUT/pytest_hboth.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_hboth.log; exit 1; }
+tail -1 $OUT/pytest_hboth.log
+for r in 1 2; do
+for L in libtqr.so libtqr_hst2.so libtqr_hld18.so libtqr_hboth.so; do
+  TQR_LIB=$L timeout -k 10 120 python bench.py --no-cpu-baseline --no-host-api --steps 10 --warmup 2 > $OUT/bench_${L}_$r.json 2> $OUT/bench_${L}_$r.err || { echo "bench $L failed"; tail -20 $OUT/bench_${L}_$r.err; exit 1; }
+  echo "$L $(python3 -c "import json,sys; d=json.load(open('$OUT/bench_${L}_$r.json')); print(d['ms_per_step'], d['value'], d['roofline']['frac'])")"
+done
+done
