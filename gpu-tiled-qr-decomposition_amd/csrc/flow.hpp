@@ -109,6 +109,9 @@ constexpr bool FLOW_PF = true;
 #ifndef TQR_HEAD_ST_AUX
 #define TQR_HEAD_ST_AUX 0
 #endif
+#ifndef TQR_HEAD_LD0_AUX  // (an element's first group)
+#define TQR_HEAD_LD0_AUX 16
+#endif
 #ifndef TQR_HEAD_LD_AUX
 #define TQR_HEAD_LD_AUX 18  // sc1 | nt: 129.86 vs 130.03-130.14 ms (2 A/B rounds; nt stores: 130.2, slower)
 #endif  // software-pipelined operand reads (also at 2 waves/SIMD)
@@ -766,7 +769,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     // variant with ks0-skipping cost the TSMQR phase 2 its operand prefetch), for ~1 % extra flops.
     const __amdgpu_buffer_rsrc_t hrs = head_rsrc(At + (size_t)col * ldm, ts);  // UNMQR: empty resource, head = 0
     const unsigned hoff = head_off_pair<B>(ldm, 0);
-    if (FLOW_PF && active) load_head_pair<B, 16>(H, hrs, hoff);
+    if (FLOW_PF && active) load_head_pair<B, TQR_HEAD_LD0_AUX>(H, hrs, hoff);
     FST(4);
     const int inext = (i == k) ? i0 : i + 1;
     const bool has_next = inext < i1;
