@@ -29,10 +29,10 @@
 // cache policy of the strip traffic (tile strips streamed once per step): aux bits of the buffer
 // loads / stores (16 = sc1 write-through / L1 bypass, | 2 = nt streaming)
 #ifndef TQR_STRIP_LD_AUX
-#define TQR_STRIP_LD_AUX 16
+#define TQR_STRIP_LD_AUX 18  // sc1 | nt: 129.9 vs 130.4-130.6 ms at 16384^2 (2 A/B rounds, late round 2)
 #endif
 #ifndef TQR_STRIP_ST_AUX
-#define TQR_STRIP_ST_AUX 16
+#define TQR_STRIP_ST_AUX 16  // (nt stores: 131.1, slower)
 #endif
 namespace tqr {
 
