@@ -28,8 +28,13 @@
 
 // cache policy of the strip traffic (tile strips streamed once per step): aux bits of the buffer
 // loads / stores (16 = sc1 write-through / L1 bypass, | 2 = nt streaming)
+// fp64 strips: sc1 | nt loads (16384^2: 127.7 vs 128.9-129.0 ms, two A/B rounds); fp32 strips
+// (the fp32 panels' trailing update) keep sc1 (nt: 481.5 vs 474.1-475.1 ms at 32768^2)
 #ifndef TQR_STRIP_LD_AUX
-#define TQR_STRIP_LD_AUX 18  // sc1 | nt: 129.9 vs 130.4-130.6 ms at 16384^2 (2 A/B rounds, late round 2)
+#define TQR_STRIP_LD_AUX 18
+#endif
+#ifndef TQR_STRIP_LD_AUX32
+#define TQR_STRIP_LD_AUX32 16
 #endif
 #ifndef TQR_STRIP_ST_AUX
 #define TQR_STRIP_ST_AUX 16  // (nt stores: 131.1, slower)
@@ -464,7 +469,7 @@ __device__ __forceinline__ void load_strip_pair(double (&X)[Geo<B>::NKS], S* til
       X[2 * h] = __longlong_as_double(((long long)v[1] << 32) | v[0]);
       X[2 * h + 1] = __longlong_as_double(((long long)v[3] << 32) | v[2]);
     } else {
-      auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, base, so, TQR_STRIP_LD_AUX);
+      auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, base, so, TQR_STRIP_LD_AUX32);
       X[2 * h] = (double)__uint_as_float(v[0]);
       X[2 * h + 1] = (double)__uint_as_float(v[1]);
     }

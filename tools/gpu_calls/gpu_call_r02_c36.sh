@@ -1,10 +1,14 @@
+# final HEAD (nt strip + head loads): full GPU suite, default bench, rocprof kernel stats, fp32 c5 bench
 set -o pipefail
-mkdir -p gpurun_out/r02_c36
-timeout -k 10 400 python -u -m pytest tests -q -x -m gpu --timeout 300 --timeout-method thread -k "not 65536 and not 32768 and not f32" > gpurun_out/r02_c36/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "^FAILED|passed|failed" gpurun_out/r02_c36/pytest_gpu.log; tail -30 gpurun_out/r02_c36/pytest_gpu.log; exit 1; }
-tail -1 gpurun_out/r02_c36/pytest_gpu.log
-for v in libtqr.so libtqr_sync.so libtqr.so libtqr_sync.so; do
-  TQR_LIB=$v timeout -k 10 200 python bench.py --no-cpu-baseline --no-host-api --steps 10 > gpurun_out/r02_c36/bench_$v.json 2> gpurun_out/r02_c36/bench_$v.err || { echo bench failed; tail gpurun_out/r02_c36/bench_$v.err; exit 1; }
-  python3 -c "import json;d=json.loads(open('gpurun_out/r02_c36/bench_$v.json').read());print('$v', d['ms_per_step'], d['roofline']['frac'])"
-done
-TQR_FST_LIB=libtqr_fst.so timeout -k 10 200 python tools/flowstamps.py 16384 > gpurun_out/r02_c36/fst.txt 2>&1 || { echo "fst failed"; tail gpurun_out/r02_c36/fst.txt; exit 1; }
-grep -E "wall|wave" gpurun_out/r02_c36/fst.txt
+OUT=gpurun_out/c36; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -q -x -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+timeout -k 10 400 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { echo "bench default failed"; tail -20 $OUT/bench_default.err; exit 1; }
+python3 -c "import json; d=json.load(open('$OUT/bench_default.json')); print('default', d['ms_per_step'], d['value'], d['roofline']['frac'], d['roofline']['avg_launch_ms'], d['check'])"
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-api > $OUT/bench_10.json 2> $OUT/bench_10.err || { echo "bench 10 failed"; tail -20 $OUT/bench_10.err; exit 1; }
+python3 -c "import json; d=json.load(open('$OUT/bench_10.json')); print('steps10', d['ms_per_step'], d['value'], d['roofline']['frac'])"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-host-api --steps 2 --warmup 1 > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/prof.log; exit 1; }
+grep k_flow $OUT/prof/prof_kernel_stats.csv | cut -c1-200
+timeout -k 10 300 python bench.py --storage f32 --rows 32768 --cols 32768 --no-cpu-baseline --no-host-api --steps 4 --warmup 1 > $OUT/bench_f32.json 2> $OUT/bench_f32.err || { echo "bench f32 failed"; tail -20 $OUT/bench_f32.err; exit 1; }
+python3 -c "import json; d=json.load(open('$OUT/bench_f32.json')); print('f32 c5', d['ms_per_step'], d['value'], d['roofline']['frac'], d['check'])"

@@ -1,10 +1,12 @@
+# fp32 c5 and fp64 c3: nt strip loads (HEAD) vs sc1 strip loads, A/B x2 on one box
 set -o pipefail
-mkdir -p gpurun_out/r02_c37
-timeout -k 10 400 python -u -m pytest tests -q -x -m gpu --timeout 300 --timeout-method thread -k "not 65536 and not 32768 and not f32" > gpurun_out/r02_c37/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "^FAILED|passed|failed" gpurun_out/r02_c37/pytest_gpu.log; tail -30 gpurun_out/r02_c37/pytest_gpu.log; exit 1; }
-tail -1 gpurun_out/r02_c37/pytest_gpu.log
-for v in libtqr.so libtqr_x2.so libtqr.so libtqr_x2.so; do
-  TQR_LIB=$v timeout -k 10 200 python bench.py --no-cpu-baseline --no-host-api --steps 10 > gpurun_out/r02_c37/bench_$v.json 2> gpurun_out/r02_c37/bench_$v.err || { echo bench failed; tail gpurun_out/r02_c37/bench_$v.err; exit 1; }
-  python3 -c "import json;d=json.loads(open('gpurun_out/r02_c37/bench_$v.json').read());print('$v', d['ms_per_step'], d['roofline']['frac'])"
+OUT=gpurun_out/c37; mkdir -p $OUT
+export TMPDIR=/tmp
+for r in 1 2; do
+for L in libtqr.so libtqr_sld16.so; do
+  TQR_LIB=$L timeout -k 10 200 python bench.py --storage f32 --rows 32768 --cols 32768 --no-cpu-baseline --no-host-api --steps 4 --warmup 1 > $OUT/f32_${L}_$r.json 2> $OUT/f32_${L}_$r.err || { echo "bench f32 $L failed"; tail -20 $OUT/f32_${L}_$r.err; exit 1; }
+  echo "f32 $L $(python3 -c "import json,sys; d=json.load(open('$OUT/f32_${L}_$r.json')); print(d['ms_per_step'], d['value'], d['roofline']['frac'])")"
+  TQR_LIB=$L timeout -k 10 120 python bench.py --no-cpu-baseline --no-host-api --steps 10 --warmup 2 > $OUT/f64_${L}_$r.json 2> $OUT/f64_${L}_$r.err || { echo "bench f64 $L failed"; tail -20 $OUT/f64_${L}_$r.err; exit 1; }
+  echo "f64 $L $(python3 -c "import json,sys; d=json.load(open('$OUT/f64_${L}_$r.json')); print(d['ms_per_step'], d['value'], d['roofline']['frac'])")"
 done
-TQR_FST_LIB=libtqr_fst.so timeout -k 10 200 python tools/flowstamps.py 16384 > gpurun_out/r02_c37/fst.txt 2>&1 || { echo "fst failed"; tail gpurun_out/r02_c37/fst.txt; exit 1; }
-grep -E "wall|wave" gpurun_out/r02_c37/fst.txt
+done
