@@ -1,6 +1,6 @@
 # final HEAD (nt strip + head loads): full GPU suite, default bench, rocprof kernel stats, fp32 c5 bench
 set -o pipefail
-OUT=gpurun_out/c36; mkdir -p $OUT
+OUT=${OUT:-gpurun_out/c36}; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -q -x -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
