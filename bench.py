@@ -170,6 +170,38 @@ def check_owned_columns(A0, A, m, n, b, rank, world):
     return rel
 
 
+def single_gpu_leg(tqr, torch, m, n, b, dt, steps, warmup):
+    """t(1 GPU) of the strong-scaling ratio: the N > 1 workload on this GPU alone, timed like the
+    N-rank leg (staged inputs when steps copies fit in 96 GiB, else a restore inside each step)."""
+    A0 = torch.empty((n, m), dtype=dt, device="cuda")
+    tqr.fill_randzo(A0, m, n, 5)
+    A = A0.clone()
+    tau = torch.zeros((min(m, n) // b, m), dtype=dt, device="cuda")
+    plan = tqr.TiledQR(m, n, b, dt)
+    staged = steps * A0.numel() * A0.element_size() <= (96 << 30)
+    As = [A0.clone() for _ in range(steps)] if staged else []
+    for _ in range(warmup):
+        A.copy_(A0)
+        plan.execute(A, tau)
+    torch.cuda.synchronize()
+    plan.status()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        if staged:
+            plan.execute(As[s], tau)
+        else:
+            A.copy_(A0)
+            plan.execute(A, tau)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    plan.status()
+    rel = check_output(A0, As[-1] if staged and steps else A, m, n)
+    del As, A, A0, tau, plan
+    torch.cuda.empty_cache()
+    return {"t1_ms": round(el / steps * 1e3, 3), "t1_inputs": "staged" if staged else "restored in step",
+            "t1_column_norm_rel_err": rel}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -186,6 +218,8 @@ def main():
     ap.add_argument("--no-host-api", action="store_true",
                     help="skip the PCIe-inclusive host-pointer timing (tqr_*geqrt_host)")
     ap.add_argument("--cpu-sample", type=int, default=6144)
+    ap.add_argument("--no-single-leg", action="store_true",
+                    help="N > 1: skip rank 0's single-GPU timing of the same matrix (strong_scaling)")
     args = ap.parse_args()
 
     import torch
@@ -210,6 +244,15 @@ def main():
     b = args.tile
     dt = torch.float64 if args.storage == "f64" else torch.float32
     q = n // b
+    rehearsal = world > 1 and "TQR_BENCH_DEVICE" in os.environ
+
+    # strong scaling, self-contained: before the N-rank region, rank 0 factorises the same m x n
+    # matrix on its GPU alone (single-GPU engine, same steps / warmup / input handling); the others wait
+    single = None
+    if dist:
+        if rank == 0 and not args.no_single_leg:
+            single = single_gpu_leg(tqr, torch, m, n, b, dt, args.steps, args.warmup)
+        dist.barrier()
 
     A0 = torch.empty((n, m), dtype=dt, device="cuda")
     tqr.fill_randzo(A0, m, n, 5)
@@ -280,6 +323,15 @@ def main():
         dist.all_gather_object(ranks, mine)
         dist_info = {"world_size": world, "ranks": ranks}
     ms_step = el / args.steps * 1e3
+    strong = None
+    if single:
+        strong = dict(single, tN_ms=round(ms_step, 3), tN_inputs="staged" if staged else "restored in step",
+                      speedup=round(single["t1_ms"] / ms_step, 3),
+                      efficiency=round(single["t1_ms"] / ms_step / world, 3),
+                      note="t1: the same matrix on rank 0's GPU alone (single-GPU engine), timed before the "
+                           f"{world}-rank region with the same steps, warmup and input handling" +
+                           ("; REHEARSAL: all ranks share one GPU (TQR_BENCH_DEVICE), so this is not a "
+                            "multi-GPU measurement" if rehearsal else ""))
     total_flops = qr_flops(m, n) * args.steps
     value = total_flops / el / 1e9
 
@@ -319,19 +371,33 @@ def main():
         # the reference's calling convention (host matrix in, factorised host matrix out): pageable
         # host array -> pinned staging -> HBM, factorisation, and back (outside the timed region;
         # reported beside, never as, the value)
+        import numpy as np
         Ah = A0.cpu().numpy()
-        times = []
-        for _ in range(2):
-            F = Ah.copy()
-            t0 = time.perf_counter()
-            tqr.geqrt_host(F, b)
-            times.append(time.perf_counter() - t0)
-        th = min(times)
-        host_api = {"ms": round(th * 1e3, 1), "gflops": round(qr_flops(m, n) / th / 1e9, 1),
+        Th = np.zeros_like(Ah)  # the caller's zeroed tau matrix (qrdecomp.c:90), allocated beforehand
+
+        def host_ms(with_tau, mode):
+            os.environ["TQR_HOST_XFER"] = mode
+            times = []
+            for _ in range(3):
+                F = Ah.copy()
+                t0 = time.perf_counter()
+                tqr.geqrt_host(F, b, with_tau=with_tau, tau=Th if with_tau else None)
+                times.append(time.perf_counter() - t0)
+            os.environ.pop("TQR_HOST_XFER", None)
+            return min(times) * 1e3
+
+        th = host_ms(True, "stage")
+        th_nt = host_ms(False, "stage")
+        th_reg = host_ms(False, "register")
+        host_api = {"ms": round(th, 1), "gflops": round(qr_flops(m, n) / th / 1e6, 1),
+                    "ms_no_tau": round(th_nt, 1), "ms_registered_no_tau": round(th_reg, 1),
                     "h2d_d2h_bytes": 2 * Ah.nbytes,
-                    "note": "tqr_geqrt_host end to end: pageable host array, pinned double-buffered staging, "
-                            "async copies, factorisation, copies back, tau expanded to m x n"}
-        del Ah, F
+                    "note": "tqr_geqrt_host end to end (best of 3), pageable host array in, factorised array "
+                            "(+ the reference's m x n tau matrix for 'ms') out; the persistent launch uploads each "
+                            "tile column before step 0 needs it and downloads it once final (csrc/xfer.hpp), host "
+                            "threads filling / draining a pinned staging buffer meanwhile; ms_registered_no_tau: the "
+                            "caller's array page-locked for the call and read / written by the launch directly"}
+        del Ah, Th
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample, 256)
@@ -355,13 +421,16 @@ def main():
             "data": "synthetic (RANDZO distribution, device-generated)",
             "config": {"workload": f"tiled QR {m}x{n} {args.storage} storage, tile {b} (BASELINE configs[{cfg}])", "m": m, "n": n,
                        "tile": b, "parallelism": "single GPU" if world == 1 else
-                       f"{world} GPUs, tile-column cyclic, panel V/T forwarded over xGMI",
+                       (f"{world} ranks on ONE GPU (rehearsal, TQR_BENCH_DEVICE), tile-column cyclic, panel V/T "
+                        "forwarded device to device" if rehearsal else
+                        f"{world} GPUs, tile-column cyclic, panel V/T forwarded over xGMI"),
                        "inputs": "one resident copy per timed step, staged before the timed region" if staged
                        else "input restored by a device copy inside each timed step"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "check": {"column_norm_rel_err": ok_rel} if ok_rel is not None else None,
             "dist": dist_info,
+            "strong_scaling": strong,
             "host_api": host_api,
         }
         print(json.dumps(line))

@@ -286,6 +286,10 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
   };
   const Strip32<B> hs(At, ldm, col);  // the head tile's strip
   FST(6);
+  if (k == 0 && a.Uc) {  // host-pointer API: tile column j uploaded (xfer.hpp)
+    const bool ok = t == FLOW_PT ? spin_ge(&a.Uc[j], a.nxc, err) : true;
+    if (!wg_verdict(ok, sflag)) return;
+  }
   const int ifirst = seg == 0 ? k : i0;
   for (int i = ifirst; i < i1 || i == k; i = (i == k ? i0 : i + 1)) {
     const bool ts = i != k;

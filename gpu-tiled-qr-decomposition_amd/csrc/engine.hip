@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -347,20 +348,35 @@ struct FlowPlan {
 //                       segment holding row k; for each of its rows i: panel (i,k) and the
 //                       step-(k-1) segment holding row i.
 // Segment boundaries are read from the list itself (any segment lengths).
+// Host-pointer API lists (xfer.hpp) also hold UP(j, c) / DOWN(j, c): every step-0 task of tile
+// column j (GEQRT(0) / TSQRT(i, 0) for j = 0, the chains of step 0 on j) must come after all
+// UP(j, *); DOWN(j, c) after every chain of a step k < j on column j and every panel task of step j.
 static bool flow_list_topological(const std::vector<Item>& L, int p, int q, int ns) {
   std::map<std::pair<int, int>, int> ppos;                       // (i, k) -> position
   std::map<std::tuple<int, int, int, int>, int> cpos;            // (k, j, s, e) -> position
   std::map<std::tuple<int, int, int, int>, int> rowpos;          // (k, j, s, row) -> position
+  std::map<std::pair<int, int>, int> upos, dpos;                 // (j, c) -> position
+  std::vector<int> uplast(q, -1);                                // last UP(j, *) of column j
+  std::vector<int> collast(q, -1);                               // last task DOWN(j, *) waits for
   for (int x = 0; x < (int)L.size(); ++x) {
     const Item& it = L[x];
     const int ty = it.ts & 0xff;
     if (ty == T_CHAIN) {
       const int s = (it.ts >> 8) & 0xff, k = it.k & 0xffff, e = it.k >> 16, j = it.m, i0 = it.l & 0xffff, i1 = it.l >> 16;
+      if (j < 0 || j >= q) return false;
       if (!cpos.emplace(std::make_tuple(k, j, s, e), x).second) return false;
       if (e == 0) rowpos[std::make_tuple(k, j, s, k)] = x;
       for (int i = i0; i < i1; ++i) rowpos[std::make_tuple(k, j, s, i)] = x;
+      if (k < j) collast[j] = std::max(collast[j], x);
     } else if (ty == QRS || ty == QRD) {
+      if (it.k < 0 || it.k >= q) return false;
       if (!ppos.emplace(std::make_pair(it.l, it.k), x).second) return false;
+      collast[it.k] = std::max(collast[it.k], x);
+    } else if (ty == T_UP || ty == T_DOWN) {
+      if (it.m < 0 || it.m >= q) return false;
+      auto& mp = ty == T_UP ? upos : dpos;
+      if (!mp.emplace(std::make_pair(it.m, (it.ts >> 8) & 0xff), x).second) return false;
+      if (ty == T_UP) uplast[it.m] = std::max(uplast[it.m], x);
     } else {
       return false;
     }
@@ -369,6 +385,16 @@ static bool flow_list_topological(const std::vector<Item>& L, int p, int q, int 
     auto f = mp.find(key);
     return f != mp.end() && f->second < x;
   };
+  const bool xfer = !upos.empty();
+  if (xfer) {  // every column uploaded and downloaded by the same number of chunks
+    const int nxc = (int)upos.size() / q;
+    if ((int)upos.size() != nxc * q || dpos.size() != upos.size()) return false;
+    for (int j = 0; j < q; ++j)
+      for (int c = 0; c < nxc; ++c)
+        if (!upos.count(std::make_pair(j, c)) || !dpos.count(std::make_pair(j, c))) return false;
+  } else if (!dpos.empty()) {
+    return false;
+  }
   for (int x = 0; x < (int)L.size(); ++x) {
     const Item& it = L[x];
     const int ty = it.ts & 0xff;
@@ -377,30 +403,49 @@ static bool flow_list_topological(const std::vector<Item>& L, int p, int q, int 
       if (e > 0 && !before(cpos, std::make_tuple(k, j, s, e - 1), x)) return false;
       if (e == 0 && !before(ppos, std::make_pair(k, k), x)) return false;
       if (e == 0 && k > 0 && !before(rowpos, std::make_tuple(k - 1, j, s, k), x)) return false;
+      if (xfer && k == 0 && !(uplast[j] < x)) return false;
       for (int i = i0; i < i1; ++i) {
         if (!before(ppos, std::make_pair(i, k), x)) return false;
         if (k > 0 && !before(rowpos, std::make_tuple(k - 1, j, s, i), x)) return false;
       }
-    } else {
+    } else if (ty == T_DOWN) {
+      if (!(collast[it.m] < x)) return false;
+    } else if (ty == QRS || ty == QRD) {
       const int i = it.l, k = it.k;
       if (i > k && !before(ppos, std::make_pair(i - 1, k), x)) return false;
+      if (xfer && k == 0 && !(uplast[0] < x)) return false;
       if (k > 0)
         for (int s = 0; s < ns; ++s)
           if (!before(rowpos, std::make_tuple(k - 1, k, s, i), x)) return false;
     }
   }
-  (void)p; (void)q;
+  (void)p;
   return true;
 }
 
-static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp) {
-  const int kmax = std::min(p, q), ns = (b + FLOW_SW - 1) / FLOW_SW, ng = b / (b < 32 ? b : 32);
-  // segment length per chain: the lookahead column (j = k+1, the DAG's critical path: its chain
-  // elements feed the next panel's members) may use shorter segments (TQR_SEGLEN_LA), which
-  // pipeline consecutive elements on different workgroups at reflector-group granularity
+// Host-pointer API: the persistent launch also carries the transfers (xfer.hpp). nxc chunks per
+// tile column; tcol = one column's upload time in the estimator's unit (a chain element).
+struct XferPlan {
+  int nxc = 0;
+  double tcol = 0.0;
+};
+
+// chain segment length of the lookahead column (j = k+1, the DAG's critical path: its chain
+// elements feed the next panel's members): TQR_SEGLEN_LA, else the plan's seglen
+static int seglen_la_of(int seglen) {
   const char* esl = getenv("TQR_SEGLEN_LA");
-  const int seglen_la = esl ? std::max(1, atoi(esl)) : seglen_;
+  return esl ? std::max(1, atoi(esl)) : seglen;
+}
+
+static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp, const XferPlan* xp = nullptr) {
+  const int kmax = std::min(p, q), ns = (b + FLOW_SW - 1) / FLOW_SW, ng = b / (b < 32 ? b : 32);
+  // segment length per chain: shorter segments for the lookahead column pipeline consecutive
+  // elements on different workgroups at reflector-group granularity
+  const int seglen_la = seglen_la_of(seglen_);
   auto seglen_of = [&](int k, int j) { return j == k + 1 ? seglen_la : seglen_; };
+  // host-pointer API: tile column j arrives (uploaded) at arrive(j); step-0 tasks start after it
+  const bool xfer = xp && xp->nxc > 0;
+  auto arrive = [&](int j) { return xfer ? (j + 1) * xp->tcol : 0.0; };
   // cost model (unit: one chain element): Tg = one panel group-step; tunable for experiments
   const char* eg = getenv("TQR_TG");
   const double Tg = eg ? atof(eg) : 1.4, Te = 1.0;
@@ -418,9 +463,12 @@ static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp) {
   auto fin_prev = [&](int k, int i, int j) { return k > 0 ? fin[id3(k - 1, i, j)] : 0.0; };
   struct T { double est; int ord; Item it; };
   std::vector<T> tl;
+  if (xfer)  // uploads, in column order (one column's chunks together: they share the link)
+    for (int j = 0; j < q; ++j)
+      for (int c = 0; c < xp->nxc; ++c) tl.push_back({arrive(j) - xp->tcol, -1, Item{T_UP | (c << 8), 0, j, 0}});
   for (int k = 0; k < kmax; ++k) {
     // panel
-    double ps = fin_prev(k, k, k);
+    double ps = std::max(fin_prev(k, k, k), k == 0 ? arrive(0) : 0.0);
     pstart[(size_t)k * p + k] = ps;
     tl.push_back({ps - la, 0, Item{QRS, k, k, k}});
     for (int i = k + 1; i < p; ++i) {
@@ -430,7 +478,7 @@ static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp) {
     }
     // chains
     for (int j = k + 1; j < q; ++j) {
-      double t0 = std::max(fin_prev(k, k, j), pstart[(size_t)k * p + k] + Tg);
+      double t0 = std::max({fin_prev(k, k, j), pstart[(size_t)k * p + k] + Tg, k == 0 ? arrive(j) : 0.0});
       double prev = t0 + 0.5 * Te;  // UNMQR
       fin[id3(k, k, j)] = prev;
       std::vector<double> seg_start;
@@ -460,7 +508,15 @@ static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp) {
       }
     }
   }
-  // bump every task's key past its dependencies' keys (tl is topological, step-major), so the
+  if (xfer) {  // downloads: when tile column j is final (its last chain element, its panel)
+    for (int j = 0; j < q; ++j) {
+      double cf = 0.0;
+      for (int k = 0; k < std::min(j, kmax); ++k) cf = std::max(cf, fin[id3(k, p - 1 > k ? p - 1 : k, j)]);
+      if (j < kmax) cf = std::max(cf, pstart[(size_t)j * p + p - 1] + ng * Tg);
+      for (int c = 0; c < xp->nxc; ++c) tl.push_back({cf, 2, Item{T_DOWN | (c << 8), 0, j, 0}});
+    }
+  }
+  // bump every task's key past its dependencies' keys (tl is topological), so the
   // estimated-time order is topological by construction
   {
     std::map<std::tuple<int, int, int, int, int>, int> idx;
@@ -468,26 +524,42 @@ static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp) {
       const Item& it = tl[x].it;
       int ty = it.ts & 0xff;
       if (ty == T_CHAIN) idx[std::make_tuple(T_CHAIN, it.k & 0xffff, it.m, (it.ts >> 8) & 0xff, it.k >> 16)] = x;
+      else if (ty == T_UP || ty == T_DOWN) idx[std::make_tuple(ty, it.m, (it.ts >> 8) & 0xff, 0, 0)] = x;
       else idx[std::make_tuple(0, it.l, it.k, 0, 0)] = x;
     }
     auto seg_of = [&](int k, int j, int i) { return (i - k - 1) / seglen_of(k, j); };
+    auto nseg_of = [&](int k, int j) { return p - k - 1 > 0 ? (p - k - 1 + seglen_of(k, j) - 1) / seglen_of(k, j) : 1; };
     for (int x = 0; x < (int)tl.size(); ++x) {
       const Item& it = tl[x].it;
       int ty = it.ts & 0xff;
       double key = tl[x].est;
       auto bump = [&](int d) { key = std::max(key, tl[d].est + 1e-6); };
+      auto bump_up = [&](int j) {
+        if (xfer)
+          for (int c = 0; c < xp->nxc; ++c) bump(idx[std::make_tuple(T_UP, j, c, 0, 0)]);
+      };
       if (ty == T_CHAIN) {
         int s = (it.ts >> 8) & 0xff, k = it.k & 0xffff, e = it.k >> 16, j = it.m, i0 = it.l & 0xffff, i1 = it.l >> 16;
         if (e > 0) bump(idx[std::make_tuple(T_CHAIN, k, j, s, e - 1)]);
         else bump(idx[std::make_tuple(0, k, k, 0, 0)]);
         if (e == 0 && k > 0) bump(idx[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, j, k))]);
+        if (k == 0) bump_up(j);
         for (int i = i0; i < i1; ++i) {
           bump(idx[std::make_tuple(0, i, k, 0, 0)]);
           if (k > 0) bump(idx[std::make_tuple(T_CHAIN, k - 1, j, s, seg_of(k - 1, j, i))]);
         }
+      } else if (ty == T_UP) {
+      } else if (ty == T_DOWN) {
+        const int j = it.m;
+        for (int k = 0; k < std::min(j, kmax); ++k)
+          for (int s = 0; s < ns; ++s)
+            for (int e = 0; e < nseg_of(k, j); ++e) bump(idx[std::make_tuple(T_CHAIN, k, j, s, e)]);
+        if (j < kmax)
+          for (int i = j; i < p; ++i) bump(idx[std::make_tuple(0, i, j, 0, 0)]);
       } else {
         int i = it.l, k = it.k;
         if (i > k) bump(idx[std::make_tuple(0, i - 1, k, 0, 0)]);
+        if (k == 0) bump_up(0);
         if (k > 0)
           for (int s = 0; s < ns; ++s) bump(idx[std::make_tuple(T_CHAIN, k - 1, k, s, seg_of(k - 1, k, i))]);
       }
@@ -619,15 +691,31 @@ struct tqr_plan {
   // mutex around each enqueue sequence, and every execute's stream waits for the previous one
   std::mutex mu;
   hipEvent_t evDone = nullptr;
-  // host-pointer path (geqrt_host): device buffers and two pinned staging buffers, kept with the
-  // (cached) plan; hmu serialises whole host-API calls on one plan
+  int seglen = 8, seglen_la = 8;  // chain segment lengths of the flow list (lookahead column: _la)
+  // host-pointer path (geqrt_host): device matrix and compact tau, kept with the (cached) plan
+  // (tqr_cache_clear releases them); hmu serialises whole host-API calls on one plan. The flow
+  // engine's transfers run inside its launch (xfer.hpp): a second task list with UP / DOWN
+  // tasks (d_flow_x), nxc chunks of xrows rows per tile column. The wave engine stages through
+  // two pinned buffers (pin, pev, sC) before / after its launches.
   std::mutex hmu;
   void* hA = nullptr;
   void* hT = nullptr;
+  Item* d_flow_x = nullptr;
+  int nflow_x = 0, nxc = 0, xrows = 0;
   void* pin[2] = {nullptr, nullptr};
   size_t pin_bytes = 0;
   hipStream_t sC = nullptr;
   hipEvent_t pev[2] = {nullptr, nullptr};
+};
+
+// transfer arguments of one host-pointer execute of the flow engine (xfer.hpp)
+struct XferArgs {
+  const void* hsrc;
+  void* hdst;
+  long hld;
+  int* hup;  // device view of the host flags (or null)
+  int* hdn;
+  int gen;
 };
 
 #define HIPCHK(x)                                                                         \
@@ -692,6 +780,7 @@ void tqr_plan_destroy(tqr_plan* pl) {
   if (pl->evDone) (void)hipEventDestroy(pl->evDone);
   if (pl->hA) (void)hipFree(pl->hA);
   if (pl->hT) (void)hipFree(pl->hT);
+  if (pl->d_flow_x) (void)hipFree(pl->d_flow_x);
   for (int x = 0; x < 2; ++x) {
     if (pl->pin[x]) (void)hipHostFree(pl->pin[x]);
     if (pl->pev[x]) (void)hipEventDestroy(pl->pev[x]);
@@ -796,12 +885,15 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
   if (pl->engine == TQR_ENGINE_FLOW) {
     FlowPlan fp;
     const char* sl = getenv("TQR_SEGLEN");
-    build_flow_plan(pl->p, pl->q, b, sl ? std::max(1, atoi(sl)) : 8, fp);
+    pl->seglen = sl ? std::max(1, atoi(sl)) : 8;
+    pl->seglen_la = seglen_la_of(pl->seglen);
+    build_flow_plan(pl->p, pl->q, b, pl->seglen, fp);
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
+    // next, err, Rc, Tc, Ac, Rt, Rr, then Uc (upload chunks per tile column, host-pointer API)
     pl->sync_ints = 2 + 3 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns +
-                    (size_t)pl->kmax * pl->q * pl->ns * pl->ng;
+                    (size_t)pl->kmax * pl->q * pl->ns * pl->ng + (size_t)pl->q;
     if (pl->nflow <= 0 || hipMalloc(&pl->d_flow, sizeof(Item) * pl->nflow) != hipSuccess ||
         hipMalloc(&pl->d_sync, sizeof(int) * pl->sync_ints) != hipSuccess ||
         hipMalloc(&pl->d_wk, sizeof(double*) * pl->kmax) != hipSuccess) {
@@ -1060,6 +1152,18 @@ int tqr_flow_plan_check(int M, int N, int b, int seglen, int* ntasks, int* est_o
   return TQR_OK;
 }
 
+int tqr_flow_xfer_plan_check(int M, int N, int b, int seglen, int nxc, double tcol, int* ntasks, int* est_order) {
+  if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1 || nxc < 1 || nxc > 255 || !(tcol >= 0.0)) return TQR_EINVAL;
+  FlowPlan fp;
+  XferPlan xp;
+  xp.nxc = nxc;
+  xp.tcol = tcol;
+  build_flow_plan(M, N, b, seglen, fp, &xp);
+  if (ntasks) *ntasks = (int)fp.items.size();
+  if (est_order) *est_order = fp.est_order;
+  return TQR_OK;
+}
+
 int tqr_plan_info(const tqr_plan* pl, int* engine, int* ntasks, int* est_order, int* grid) {
   if (!pl) return TQR_EINVAL;
   if (engine) *engine = pl->engine;
@@ -1084,23 +1188,36 @@ int tqr_plan_stats(const tqr_plan* pl, int* nu, double* msu, int* np, double* ms
   return TQR_OK;
 }
 
-static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_t cs);
+static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_t cs, const XferArgs* xa = nullptr);
+// Serialised enqueue of one execute (see tqr.h): the stream first waits for the plan's previous
+// execute; evDone marks this one. If enqueuing fails part-way, evDone is still recorded behind
+// whatever was enqueued (the wave engine's side streams are joined first), so the next execute
+// stays ordered after it.
+static int plan_execute_serial(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_t cs, const XferArgs* xa) {
+  std::lock_guard<std::mutex> lk(pl->mu);
+  HIPCHK(hipStreamWaitEvent(cs, pl->evDone, 0));  // the previous execute of this plan (any stream)
+  int st = plan_execute(pl, dA, ldda, dtau, cs, xa);
+  if (st != TQR_OK && pl->engine != TQR_ENGINE_FLOW) {
+    (void)hipStreamWaitEvent(cs, pl->evP, 0);
+    (void)hipStreamWaitEvent(cs, pl->evU, 0);
+  }
+  const hipError_t e = hipEventRecord(pl->evDone, cs);
+  if (st == TQR_OK && e != hipSuccess) HIPCHK(e);
+  return st;
+}
 int tqr_plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, void* stream) {
   if (!pl || !dA || !dtau || ldda < pl->m || !valid_ld(ldda, pl->es)) return TQR_EINVAL;
   // a multi-GPU plan whose peers were never imported would dereference unset peer pointers
   if (pl->world > 1 && !pl->imported) return TQR_EINVAL;
-  hipStream_t cs = (hipStream_t)stream;
-  std::lock_guard<std::mutex> lk(pl->mu);
-  HIPCHK(hipStreamWaitEvent(cs, pl->evDone, 0));  // the previous execute of this plan (any stream)
-  int st = plan_execute(pl, dA, ldda, dtau, cs);
-  if (st == TQR_OK) HIPCHK(hipEventRecord(pl->evDone, cs));
-  return st;
+  return plan_execute_serial(pl, dA, ldda, dtau, (hipStream_t)stream, nullptr);
 }
-static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_t cs) {
+static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_t cs, const XferArgs* xa) {
   if (pl->engine == 1) {
-    if (!pl->kflow || !pl->d_flow || !pl->d_sync) return TQR_EINVAL;
+    if (!pl->kflow || !pl->d_flow || !pl->d_sync || (xa && !pl->d_flow_x)) return TQR_EINVAL;
     FlowArgs f;
-    f.A = dA; f.tau = dtau; f.Wk = pl->d_wk; f.tasks = pl->d_flow; f.ntasks = pl->nflow; f.ldm = ldda;
+    f.A = dA; f.tau = dtau; f.Wk = pl->d_wk; f.ldm = ldda;
+    f.tasks = xa ? pl->d_flow_x : pl->d_flow;
+    f.ntasks = xa ? pl->nflow_x : pl->nflow;
     f.m = pl->m; f.p = pl->p; f.q = pl->q; f.kmax = pl->kmax; f.ns = pl->ns;
     f.next = pl->d_sync; f.err = pl->d_sync + 1; f.Rc = pl->d_sync + 2;
     f.Tc = f.Rc + (size_t)pl->kmax * pl->ng;
@@ -1108,6 +1225,15 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     f.Rt = f.Ac + (size_t)pl->kmax * pl->q * pl->ns * pl->ng;
     f.Rr = f.Rt + (size_t)pl->kmax * pl->ng;
     f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.peers = pl->d_peers; f.Rf = pl->d_rf;
+    f.seglen = pl->seglen; f.seglen_la = pl->seglen_la;
+    if (xa) {
+      f.hsrc = xa->hsrc; f.hdst = xa->hdst; f.hld = xa->hld; f.hup = xa->hup; f.hdn = xa->hdn; f.gen = xa->gen;
+      f.Uc = f.Rr + (size_t)pl->kmax * pl->ng;
+      f.nxc = pl->nxc; f.xrows = pl->xrows;
+    } else {
+      f.hsrc = nullptr; f.hdst = nullptr; f.hld = 0; f.hup = nullptr; f.hdn = nullptr; f.gen = 0;
+      f.Uc = nullptr; f.nxc = 0; f.xrows = 0;
+    }
     // multi-GPU: counters and flags are reset by tqr_dist_reset (all ranks, then a barrier)
     if (pl->world == 1) HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
     if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
@@ -1207,48 +1333,101 @@ int tqr_sgeqrt_tiled(int m, int n, int b, float* dA, int ldda, float* dtau, void
 }
 
 // Host-pointer factorisation (the reference's calling convention: cudaQRTask copies a host matrix
-// in and out, gpucalc.cu:1614-1619, 1665-1670 — one cudaMemcpy per column). Here the transfers go
-// through two pinned staging buffers of the (cached) plan: the host copies column blocks into one
-// while the DMA engine moves the other (hipMemcpyAsync on the plan's copy stream), the factorisation
-// is stream-ordered behind the last upload, and the results come back the same way. The device
-// buffers stay with the plan (no allocation per call). tau is expanded to the reference's m x n
-// layout (column k*b of tau = compact column k).
+// in and out, gpucalc.cu:1614-1619, 1665-1670 — one cudaMemcpy per column, before and after the
+// kernel). The flow engine moves the matrix INSIDE its persistent launch (xfer.hpp): UP tasks
+// read tile columns from host memory ahead of the step-0 tasks that need them, DOWN tasks write
+// each tile column back as soon as it is final, so PCIe traffic overlaps the factorisation.
+// Host memory, one of:
+//   * staging (default): a pinned, fine-grained buffer shared by all host-API calls of the device;
+//     host threads copy the caller's columns into it tile column by tile column (flag hup[j] per
+//     column, polled by the UP tasks) and copy finished chunks back out as the DOWN tasks flag them
+//     (hdn[j][c]) — while the kernel runs;
+//   * registered (TQR_HOST_XFER=register): the caller's array itself is page-locked for the call
+//     (hipHostRegister) and read / written by the launch directly; no host copies.
+// The wave engine (cudaQRFull) keeps pre/post copies through two pinned buffers of the plan.
+// The device matrix and compact tau stay with the cached plan; tqr_cache_clear releases them.
+
+// host threads for host-side copies (the GPU box exports OMP_NUM_THREADS = this job's CPU share;
+// hardware_concurrency() there is the whole machine)
+static int host_threads() {
+  const char* e = getenv("OMP_NUM_THREADS");
+  int n = e ? atoi(e) : 0;
+  if (n <= 0) n = (int)std::max(1u, std::thread::hardware_concurrency());
+  return std::min(n, 32);
+}
+
+// Run jobs on their own threads; a job whose thread cannot be created runs on the caller, after
+// the others were started (jobs are ordered so that no job waits for a later one).
+static void run_jobs(std::vector<std::function<void()>>& jobs) {
+  std::vector<std::thread> th;
+  size_t created = 0;
+  try {
+    for (; created + 1 < jobs.size(); ++created) th.emplace_back(jobs[created]);
+  } catch (...) {
+  }
+  for (size_t x = created; x < jobs.size(); ++x) jobs[x]();
+  for (auto& t : th) t.join();
+}
+
+// wave engine: device buffers + two pinned staging buffers. Everything is allocated into locals and
+// committed to the plan only when all of it succeeded (a failed call leaves the plan untouched).
 static constexpr size_t kPinBytes = 64ull << 20;
-static int host_staging(tqr_plan* pl, size_t es) {
+static int plan_host_buffers(tqr_plan* pl, size_t es) {
   if (pl->hA) return TQR_OK;
   const size_t abytes = es * (size_t)pl->m * pl->n, tbytes = es * (size_t)pl->m * pl->kmax;
-  pl->pin_bytes = std::min(kPinBytes, std::max(abytes, tbytes));
-  if (hipMalloc(&pl->hA, abytes) != hipSuccess || hipMalloc(&pl->hT, tbytes) != hipSuccess) return TQR_ENOMEM;
-  for (int x = 0; x < 2; ++x) {
-    if (hipHostMalloc(&pl->pin[x], pl->pin_bytes, hipHostMallocDefault) != hipSuccess) return TQR_ENOMEM;
-    if (hipEventCreateWithFlags(&pl->pev[x], hipEventDisableTiming) != hipSuccess) return TQR_EHIP;
+  void *hA = nullptr, *hT = nullptr;
+  if (hipMalloc(&hA, abytes) != hipSuccess || hipMalloc(&hT, tbytes) != hipSuccess) {
+    if (hA) (void)hipFree(hA);
+    return TQR_ENOMEM;
   }
-  if (hipStreamCreateWithFlags(&pl->sC, hipStreamNonBlocking) != hipSuccess) return TQR_EHIP;
+  pl->hA = hA;
+  pl->hT = hT;
+  return TQR_OK;
+}
+static int plan_pinned_staging(tqr_plan* pl, size_t es) {
+  if (pl->pin[0]) return TQR_OK;
+  const size_t bytes = std::min(kPinBytes, std::max(es * (size_t)pl->m * pl->n, es * (size_t)pl->m * pl->kmax));
+  void* pin[2] = {nullptr, nullptr};
+  hipEvent_t pev[2] = {nullptr, nullptr};
+  hipStream_t sC = nullptr;
+  int st = TQR_OK;
+  for (int x = 0; x < 2 && st == TQR_OK; ++x) {
+    if (hipHostMalloc(&pin[x], bytes, hipHostMallocDefault) != hipSuccess) st = TQR_ENOMEM;
+    else if (hipEventCreateWithFlags(&pev[x], hipEventDisableTiming) != hipSuccess) st = TQR_EHIP;
+  }
+  if (st == TQR_OK && hipStreamCreateWithFlags(&sC, hipStreamNonBlocking) != hipSuccess) st = TQR_EHIP;
+  if (st != TQR_OK) {
+    for (int x = 0; x < 2; ++x) {
+      if (pin[x]) (void)hipHostFree(pin[x]);
+      if (pev[x]) (void)hipEventDestroy(pev[x]);
+    }
+    return st;
+  }
+  for (int x = 0; x < 2; ++x) {
+    pl->pin[x] = pin[x];
+    pl->pev[x] = pev[x];
+  }
+  pl->pin_bytes = bytes;
+  pl->sC = sC;
   return TQR_OK;
 }
 
-// host-side column copies of one staging chunk, split over a few threads (one thread moves
-// ~10 GB/s; the pinned DMA runs at PCIe rate)
-static void par_columns(size_t nc, const std::function<void(size_t)>& f) {
-  const size_t nt = std::min<size_t>({nc, 8, std::max(1u, std::thread::hardware_concurrency())});
-  if (nt <= 1) {
-    for (size_t j = 0; j < nc; ++j) f(j);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (size_t t = 0; t < nt; ++t)
-    th.emplace_back([&, t] {
-      for (size_t j = t; j < nc; j += nt) f(j);
-    });
-  for (auto& x : th) x.join();
-}
-
 // copy `ncols` columns of `rows` elements between strided host memory (ld) and packed device memory
-// through the pinned buffers, double-buffered
+// through the plan's pinned buffers, double-buffered (wave engine)
 static int staged_copy(tqr_plan* pl, char* host, size_t ld, char* dev, size_t rows, size_t ncols, size_t es, bool h2d) {
   const size_t col = es * rows, per = std::max<size_t>(1, pl->pin_bytes / col);
   const size_t nchunk = (ncols + per - 1) / per;
+  const int nthr = std::min(8, host_threads());
   auto chunk = [&](size_t c, size_t& c0, size_t& nc) { c0 = c * per; nc = std::min(per, ncols - c0); };
+  auto par_columns = [&](size_t nc, const std::function<void(size_t)>& f) {
+    const size_t nt = std::min<size_t>(nc, (size_t)nthr);
+    std::vector<std::function<void()>> jobs;
+    for (size_t t = 0; t < nt; ++t)
+      jobs.push_back([&, t] {
+        for (size_t j = t; j < nc; j += nt) f(j);
+      });
+    run_jobs(jobs);
+  };
   if (h2d) {
     for (size_t c = 0; c < nchunk; ++c) {
       size_t c0, nc;
@@ -1282,6 +1461,187 @@ static int staged_copy(tqr_plan* pl, char* host, size_t ld, char* dev, size_t ro
   return TQR_OK;
 }
 
+// The pinned, fine-grained staging buffer and flag words of the flow engine's host path, one per
+// device, shared by all plans (grown on demand; tqr_cache_clear frees it). `mu` serialises the
+// host-API calls that use it.
+struct HostStage {
+  std::mutex mu;
+  char* buf = nullptr;
+  size_t bytes = 0;
+  int* flags = nullptr;  // host view: hup[q] then hdn[q * nxc]
+  int* dflags = nullptr;  // device view
+  size_t nflags = 0;
+  int gen = 0;
+  void release() {
+    if (buf) (void)hipHostFree(buf);
+    if (flags) (void)hipHostFree(flags);
+    buf = nullptr; flags = nullptr; dflags = nullptr; bytes = 0; nflags = 0;
+  }
+  int ensure(size_t need, size_t nf) {
+    if (bytes < need) {
+      if (buf) (void)hipHostFree(buf);
+      buf = nullptr; bytes = 0;
+      void* p = nullptr;
+      if (hipHostMalloc(&p, need, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return TQR_ENOMEM;
+      buf = (char*)p;
+      bytes = need;
+    }
+    if (nflags < nf) {
+      if (flags) (void)hipHostFree(flags);
+      flags = nullptr; dflags = nullptr; nflags = 0;
+      void* p = nullptr;
+      if (hipHostMalloc(&p, nf * sizeof(int), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return TQR_ENOMEM;
+      memset(p, 0, nf * sizeof(int));
+      flags = (int*)p;
+      nflags = nf;
+      gen = 0;
+      void* d = nullptr;
+      if (hipHostGetDevicePointer(&d, flags, 0) != hipSuccess) { release(); return TQR_EHIP; }
+      dflags = (int*)d;
+    }
+    return TQR_OK;
+  }
+};
+static std::map<int, HostStage*> g_stage;  // guarded by g_cache_mu
+
+static int plan_xfer_list(tqr_plan* pl) {
+  if (pl->d_flow_x) return TQR_OK;
+  // chunk rows: one UP / DOWN task moves ~8 MiB (16-B vectors, 4 columns x 4 vectors per lane in
+  // flight), a multiple of 4 rows so 16-B vectors stay whole (fp32), and
+  // at most 255 chunks per column (the task word's chunk field)
+  int xrows = std::max(4, (int)((8u << 20) / (pl->es * (size_t)pl->b)) & ~3);
+  xrows = std::min(pl->m, std::max(xrows, ((pl->m + 254) / 255 + 3) & ~3));
+  XferPlan xp;
+  xp.nxc = (pl->m + xrows - 1) / xrows;
+  // estimator unit = one chain element (4 b^2 FLOW_SW flop at ~1/256 of the chip); a tile column
+  // over PCIe at TQR_XFER_GBS (default 45 GB/s)
+  const char* eg = getenv("TQR_XFER_GBS");
+  const double gbs = eg ? std::max(1.0, atof(eg)) : 45.0;
+  const double elem_s = 4.0 * pl->b * pl->b * FLOW_SW / (pl->dtype == TQR_F64 ? 0.175e12 : 0.38e12);
+  xp.tcol = ((double)pl->m * pl->b * pl->es / (gbs * 1e9)) / elem_s;
+  FlowPlan fp;
+  build_flow_plan(pl->p, pl->q, pl->b, pl->seglen, fp, &xp);
+  Item* d = nullptr;
+  if (hipMalloc(&d, sizeof(Item) * fp.items.size()) != hipSuccess) return TQR_ENOMEM;
+  if (hipMemcpy(d, fp.items.data(), sizeof(Item) * fp.items.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return TQR_EHIP;
+  }
+  pl->d_flow_x = d;
+  pl->nflow_x = (int)fp.items.size();
+  pl->nxc = xp.nxc;
+  pl->xrows = xrows;
+  return TQR_OK;
+}
+
+// tau: compact device array -> the reference's m x n matrix (column k*b of tau = compact column k,
+// rows k*b .. m-1; other entries untouched)
+static int tau_out(tqr_plan* pl, void* tau, int ldm, size_t es, hipStream_t s) {
+  const int m = pl->m, b = pl->b, kmax = pl->kmax;
+  std::vector<char> ct(es * (size_t)m * kmax);
+  HIPCHK(hipMemcpyAsync(ct.data(), pl->hT, ct.size(), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (int k = 0; k < kmax; ++k)
+    memcpy((char*)tau + es * ((size_t)k * b * ldm + (size_t)k * b), ct.data() + es * ((size_t)k * m + (size_t)k * b),
+           es * (size_t)(m - k * b));
+  return TQR_OK;
+}
+
+static int geqrt_host_flow(tqr_plan* pl, void* A, void* tau, int ldm, size_t es) {
+  const int m = pl->m, n = pl->n, q = pl->q, b = pl->b;
+  int st;
+  if ((st = plan_host_buffers(pl, es)) || (st = plan_xfer_list(pl))) return st;
+  if (!pl->sC && hipStreamCreateWithFlags(&pl->sC, hipStreamNonBlocking) != hipSuccess) return TQR_EHIP;
+  hipStream_t s = pl->sC;
+  HIPCHK(hipMemsetAsync(pl->hT, 0, es * (size_t)m * pl->kmax, s));
+  const char* mode = getenv("TQR_HOST_XFER");
+  if (mode && strcmp(mode, "register") == 0) {
+    const size_t span = es * ((size_t)(n - 1) * ldm + m);
+    if (hipHostRegister(A, span, hipHostRegisterMapped) == hipSuccess) {
+      void* dv = nullptr;
+      if (hipHostGetDevicePointer(&dv, A, 0) != hipSuccess) {
+        (void)hipHostUnregister(A);
+        return TQR_EHIP;
+      }
+      XferArgs xa{dv, dv, ldm, nullptr, nullptr, 0};
+      st = plan_execute_serial(pl, pl->hA, m, pl->hT, s, &xa);
+      if (st == TQR_OK) st = tqr_plan_status(pl, s);
+      else (void)hipStreamSynchronize(s);
+      (void)hipHostUnregister(A);
+      if (st == TQR_OK && tau) st = tau_out(pl, tau, ldm, es, s);
+      return st;
+    }
+    (void)hipGetLastError();  // not registrable: stage instead
+  }
+  HostStage* hs;
+  {
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    auto& e = g_stage[dev];
+    if (!e) e = new (std::nothrow) HostStage();
+    if (!e) return TQR_ENOMEM;
+    hs = e;
+  }
+  std::lock_guard<std::mutex> lk(hs->mu);
+  const int nxc = pl->nxc;
+  if ((st = hs->ensure(es * (size_t)m * n, (size_t)q * (1 + nxc)))) return st;
+  void* dbuf = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&dbuf, hs->buf, 0));
+  const int gen = ++hs->gen;
+  int* hup = hs->flags;
+  int* hdn = hs->flags + q;
+  XferArgs xa{dbuf, dbuf, m, hs->dflags, hs->dflags + q, gen};
+  if ((st = plan_execute_serial(pl, pl->hA, m, pl->hT, s, &xa))) {
+    (void)hipStreamSynchronize(s);
+    return st;
+  }
+  // host side, while the launch runs: nu threads stage tile columns in order (the last one to
+  // finish a column flags it), nd threads move finished chunks back to the caller's array
+  const int nthr = host_threads();
+  const int nu = std::max(1, nthr / 2), nd = std::max(1, nthr - nu);
+  const size_t col = es * (size_t)m;
+  char* user = (char*)A;
+  std::vector<std::atomic<int>> staged(q);
+  for (auto& x : staged) x.store(0);
+  std::atomic<int> failed{0};
+  std::vector<std::function<void()>> jobs;
+  for (int t = 0; t < nu; ++t)
+    jobs.push_back([&, t] {
+      for (int j = 0; j < q; ++j) {
+        for (int c = j * b + t; c < (j + 1) * b; c += nu) memcpy(hs->buf + c * col, user + (size_t)c * ldm * es, col);
+        if (staged[j].fetch_add(1) + 1 == nu) __atomic_store_n(&hup[j], gen, __ATOMIC_RELEASE);
+      }
+    });
+  for (int t = 0; t < nd; ++t)
+    jobs.push_back([&, t] {
+      for (int j = 0; j < q; ++j) {
+        for (int c = 0; c < nxc; ++c) {
+          // the chunk's flag, or the launch ended without setting it (an engine error)
+          for (long spins = 0; __atomic_load_n(&hdn[(size_t)j * nxc + c], __ATOMIC_ACQUIRE) < gen; ++spins) {
+            if (failed.load(std::memory_order_relaxed)) return;
+            if ((spins & 255) == 255) {
+              if (hipStreamQuery(s) != hipErrorNotReady &&
+                  __atomic_load_n(&hdn[(size_t)j * nxc + c], __ATOMIC_ACQUIRE) < gen) {
+                failed.store(1);
+                return;
+              }
+              std::this_thread::yield();
+            } else {
+              __builtin_ia32_pause();
+            }
+          }
+        }
+        for (int c = j * b + t; c < (j + 1) * b; c += nd) memcpy(user + (size_t)c * ldm * es, hs->buf + c * col, col);
+      }
+    });
+  run_jobs(jobs);
+  st = tqr_plan_status(pl, s);
+  if (st == TQR_OK && failed.load()) st = TQR_EHIP;
+  if (st == TQR_OK && tau) st = tau_out(pl, tau, ldm, es, s);
+  return st;
+}
+
 static int geqrt_host(void* A, void* tau, int m, int n, int ldm, int b, int dtype, int engine = TQR_ENGINE_DEFAULT) {
   if (!A || ldm < m || !valid_b(b) || m <= 0 || n <= 0 || m % b || n % b) return TQR_EINVAL;
   tqr_plan* pl;
@@ -1289,25 +1649,15 @@ static int geqrt_host(void* A, void* tau, int m, int n, int ldm, int b, int dtyp
   if (st) return st;
   std::lock_guard<std::mutex> lk(pl->hmu);
   const size_t es = dtype == TQR_F64 ? 8 : 4;
-  const int kmax = std::min(m, n) / b;
-  if ((st = host_staging(pl, es))) return st;
+  if (pl->engine == TQR_ENGINE_FLOW) return geqrt_host_flow(pl, A, tau, ldm, es);
+  if ((st = plan_host_buffers(pl, es)) || (st = plan_pinned_staging(pl, es))) return st;
   char* dA = (char*)pl->hA;
-  char* dT = (char*)pl->hT;
   if ((st = staged_copy(pl, (char*)A, ldm, dA, m, n, es, true))) return st;
-  HIPCHK(hipMemsetAsync(dT, 0, es * (size_t)m * kmax, pl->sC));
-  if ((st = tqr_plan_execute(pl, dA, m, dT, pl->sC))) return st;
+  HIPCHK(hipMemsetAsync(pl->hT, 0, es * (size_t)m * pl->kmax, pl->sC));
+  if ((st = plan_execute_serial(pl, dA, m, pl->hT, pl->sC, nullptr))) return st;
   if ((st = tqr_plan_status(pl, pl->sC))) return st;
   if ((st = staged_copy(pl, (char*)A, ldm, dA, m, n, es, false))) return st;
-  if (tau) {
-    // compact tau (m x kmax, packed) -> the reference's m x n matrix: column k of the compact
-    // array is column k*b of tau, rows k*b .. m-1
-    std::vector<char> ct(es * (size_t)m * kmax);
-    if ((st = staged_copy(pl, ct.data(), m, dT, m, kmax, es, false))) return st;
-    for (int k = 0; k < kmax; ++k)
-      memcpy((char*)tau + es * ((size_t)k * b * ldm + (size_t)k * b), ct.data() + es * ((size_t)k * m + (size_t)k * b),
-             es * (size_t)(m - k * b));
-  }
-  return TQR_OK;
+  return tau ? tau_out(pl, tau, ldm, es, pl->sC) : TQR_OK;
 }
 
 int tqr_dgeqrt_host(double* A, double* tau, int m, int n, int ldm, int b) { return geqrt_host(A, tau, m, n, ldm, b, TQR_F64); }
@@ -1316,6 +1666,24 @@ int tqr_geqrt_host_engine(int dtype, void* A, void* tau, int m, int n, int ldm, 
   if (dtype != TQR_F32 && dtype != TQR_F64) return TQR_EINVAL;
   if (engine != TQR_ENGINE_DEFAULT && engine != TQR_ENGINE_WAVES && engine != TQR_ENGINE_FLOW) return TQR_EINVAL;
   return geqrt_host(A, tau, m, n, ldm, b, dtype, engine);
+}
+
+// Release every cached plan (the one-shot helpers' and the host API's device matrices, compact
+// tau, pinned buffers) and the host-API staging buffers. Waits for the device first.
+int tqr_cache_clear(void) {
+  if (hipDeviceSynchronize() != hipSuccess) return TQR_EHIP;
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  for (auto& kv : g_cache) tqr_plan_destroy(kv.second);
+  g_cache.clear();
+  for (auto& kv : g_stage) {
+    {
+      std::lock_guard<std::mutex> l2(kv.second->mu);
+      kv.second->release();
+    }
+    delete kv.second;
+  }
+  g_stage.clear();
+  return TQR_OK;
 }
 
 int tqr_fill_randzo(int dtype, void* dA, int m, int n, int ldda, unsigned long long seed, void* stream) {

@@ -160,6 +160,19 @@ struct FlowArgs {
   int dist, rank, world;
   const PeerBufs* peers;
   int* Rf;
+  // host-pointer API (xfer.hpp; all null / 0 on the device API): the launch uploads its input
+  // from hsrc and downloads its result to hdst (host memory, leading dimension hld) in chunks of
+  // xrows rows, nxc per tile column. hup[j] >= gen: the host staged column j (null: hsrc was
+  // ready at launch); hdn[j * nxc + c] = gen: chunk c of column j is in hdst (null: not needed).
+  // Uc[j]: upload chunks of column j done. seglen / seglen_la: the plan's chain segment lengths
+  // (the download's column-final counts).
+  const void* hsrc;
+  void* hdst;
+  long hld;
+  int* hup;
+  int* hdn;
+  int* Uc;
+  int gen, nxc, xrows, seglen, seglen_la;
 };
 
 // ---- synchronisation ---------------------------------------------------------------------
@@ -470,6 +483,75 @@ __device__ __forceinline__ void fwd_images(const FlowArgs& a, int k, size_t vo, 
   }
 }
 
+// Multi-GPU, off the member-to-member path: reflector group g-1's images are forwarded by the
+// four waves that hold no panel rows (waves 4-7) while waves 0-3 factorise group g (panel_factor),
+// one slice per reflector step — each lane loads its 16-B unit of the next slice while it stores
+// the current one to every peer — and the last of those waves to drain its stores sets the peers'
+// member flags of group g-1 (release, system scope). Before (round 2) all 512 threads copied the
+// images between group g's Rc publish and its in-tile trailing update, on the path the next member's
+// trailing waits for. The last group is still forwarded that way (no next factorisation).
+struct FwdJob {
+  const FlowArgs* a;
+  int k;
+  size_t vo, to;  // the group's V / T image offsets in workspace k (doubles)
+  size_t fo;      // its member flag index in Rf: (k * p + i) * NG + g
+  int nv, nt;     // 16-B units of the V and T images
+  int* cnt;       // LDS arrival counter of the forwarding waves (0 between uses)
+};
+
+__device__ __noinline__ void panel_idle(const FwdJob* fjp, int IB, bool TS) {
+  const FwdJob fj = *fjp;
+  const FlowArgs& a = *fj.a;
+  const int tid = threadIdx.x - 256, lane = threadIdx.x & 63;
+  const int nu = fj.nv + fj.nt, per = (nu + IB - 1) / IB;  // units per reflector step
+  // lane r holds peer r's workspace k and flag array (read once; v_readlane per use)
+  unsigned long long pw = 0, pf = 0;
+  if (lane < a.world) {
+    pw = (unsigned long long)a.peers[lane].Wk[fj.k];
+    pf = (unsigned long long)a.peers[lane].Rf;
+  }
+  // one resource per workspace (its base is wave-uniform), per-lane byte offsets: a wave's units
+  // may straddle the V / T boundary (a workspace is < 2 GiB, the IPC export bound)
+  const __amdgpu_buffer_rsrc_t sw = uniform_rsrc(a.Wk[fj.k]);
+  auto unit_off = [&](int u) -> unsigned {
+    return u < fj.nv ? (unsigned)(fj.vo * 8 + 16 * (size_t)u) : (unsigned)(fj.to * 8 + 16 * (size_t)(u - fj.nv));
+  };
+  typedef __attribute__((ext_vector_type(4))) unsigned v4u;
+  auto unit_ld = [&](int u) -> v4u { return __builtin_amdgcn_raw_buffer_load_b128(sw, unit_off(u), 0, 16); };
+  auto peer = [&](unsigned long long v, int r) {
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)v, r), hi = __builtin_amdgcn_readlane((unsigned)(v >> 32), r);
+    return (char*)(((unsigned long long)hi << 32) | lo);
+  };
+  v4u cur = {0, 0, 0, 0}, nxt = {0, 0, 0, 0};
+  if (tid < per && tid < nu) cur = unit_ld(tid);
+  for (int C = 0; C < IB; ++C) {
+    const int un = (C + 1) * per + tid, uc = C * per + tid;
+    if (C + 1 < IB && tid < per && un < nu) nxt = unit_ld(un);
+    if (tid < per && uc < nu) {
+      const unsigned off = unit_off(uc);
+      for (int r = 0; r < a.world; ++r)
+        if (r != a.rank) __builtin_amdgcn_raw_buffer_store_b128(cur, uniform_rsrc(peer(pw, r)), off, 0, 17);
+    }
+    __syncthreads();
+    cur = nxt;
+  }
+  __syncthreads();
+  if (TS) __syncthreads();
+  // every forwarding wave drains its own stores, then counts itself in; the last one signals
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(lds_int(fj.cnt), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  old = __shfl(old, 0);
+  if (old == 3 && lane == 0) {
+    *lds_int(fj.cnt) = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int r = 0; r < a.world; ++r)
+      if (r != a.rank)
+        __hip_atomic_store((int*)peer(pf, r) + fj.fo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // ---- panel tasks ---------------------------------------------------------------------------
 template <int B, typename S>
 __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* lds, int* sflag) {
@@ -491,9 +573,11 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
   S* Bt = qrs ? Rt : A + (size_t)k * B * ldm + (size_t)l * B;
   const int pos = qrs ? 0 : l - k;  // position in the panel chain
   FST(6);
-  // the tile(s) must have received step k-1 on every strip
+  // the tile(s) must have received step k-1 on every strip (step 0, host-pointer API: tile
+  // column 0 uploaded, xfer.hpp)
   {
     bool ok = true;
+    if (t == FLOW_PT && k == 0 && a.Uc) ok = spin_ge(&a.Uc[0], a.nxc, a.err);
     if (t == FLOW_PT && k > 0)
       for (int s = 0; s < a.ns && ok; ++s) ok = spin_ge(&a.Tc[((size_t)(qrs ? k : l) * a.q + k) * a.ns + s], k, a.err);
     if (!wg_verdict(ok, sflag)) return;
@@ -501,6 +585,8 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
   FST(1);
   double X[G::NKS];
   double H[G::NRI];
+  const int me = qrs ? k : l;
+  if (a.dist && t == 0) *lds_int(sflag + 36) = 0;  // the forwarding waves' arrival counter
   for (int g = 0; g < NG; ++g) {
     const int c0 = g * IB;
     if (!qrs) {  // R_kk rows of group g as left by the previous chain member
@@ -531,9 +617,13 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     FST(10);
     // Vs holds the panel rows in the chains' paired order (LDS row q = tile row vimg_row(q)): the
     // V image is then a verbatim copy and the trailing update moves 16-B row pairs
+    // multi-GPU: waves 4-7 forward group g-1's images meanwhile (FwdJob)
+    const FwdJob fj{&a, k, flow_vw_off<B, S>(a.p, me, k, g - 1), flow_tw_off<B, S>(a.p, me, k, g - 1),
+                    ((size_t)k * a.p + me) * NG + g - 1, Img<B, S>::V / 2, Img<B, S>::T / 2, sflag + 36};
+    const FwdJob* fjp = a.dist && g > 0 ? &fj : nullptr;
 #ifndef TQR_DIAG_NOPFACT  // what-if: no panel factorisation (results wrong)
-    if (qrs) panel_factor<B, false, true>(Vs, Hs, tauv, scratch, c0);
-    else panel_factor<B, true, true>(Vs, Hs, tauv, scratch, c0);
+    if (qrs) panel_factor<B, false, true>(Vs, Hs, tauv, scratch, c0, fjp);
+    else panel_factor<B, true, true>(Vs, Hs, tauv, scratch, c0, fjp);
 #endif
     FST(5);
     {  // write-back of the factored block (R / V), row pairs as 16-B write-through stores
@@ -596,8 +686,9 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
     wg_publish(&a.Rc[(size_t)k * NG + g], 1);
     FST(10);
-    // multi-GPU: the images to every peer (drained by the Rt publish below, flags after it)
-    if (a.dist) fwd_images<B, S>(a, k, flow_vw_off<B, S>(a.p, qrs ? k : l, k, g), flow_tw_off<B, S>(a.p, qrs ? k : l, k, g));
+    // multi-GPU, last group: the images to every peer now (drained by the Rt publish below, flags
+    // after it); earlier groups go during the next group's factorisation (FwdJob)
+    if (a.dist && g + 1 == NG) fwd_images<B, S>(a, k, flow_vw_off<B, S>(a.p, me, k, g), flow_tw_off<B, S>(a.p, me, k, g));
     FST(23);
     if (!qrs) {  // R_kk head rows right of the group as left by the previous member's trailing
       const bool ok = t == FLOW_PT ? spin_ge(&a.Rt[(size_t)k * NG + g], pos, a.err) : true;
@@ -635,9 +726,10 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     }
     wg_publish(&a.Rt[(size_t)k * NG + g], 1);
     FST(12);
-    if (a.dist && t == 0) {  // every wave's peer stores drained (the Rt publish): release, flags
+    if (a.dist && g + 1 == NG && t == 0) {  // every wave's peer stores drained (the Rt publish): release, flags
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
-      const size_t fo = ((size_t)k * a.p + (qrs ? k : l)) * NG + g;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const size_t fo = ((size_t)k * a.p + me) * NG + g;
       for (int r = 0; r < a.world; ++r)
         if (r != a.rank) __hip_atomic_store(&a.peers[r].Rf[fo], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -735,6 +827,10 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     return spin_ge(fp, 1, err, true);
   };
   FST(6);
+  if (k == 0 && a.Uc) {  // host-pointer API: tile column j uploaded (xfer.hpp)
+    const bool ok = t == FLOW_PT ? spin_ge(&a.Uc[j], a.nxc, err) : true;
+    if (!wg_verdict(ok, sflag)) return;
+  }
   const int ifirst = seg == 0 ? k : i0;
   for (int i = ifirst; i < i1 || i == k; i = (i == k ? i0 : i + 1)) {
     const bool ts = i != k;
@@ -915,6 +1011,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
 
 }  // namespace tqr
 #include "chain32.hpp"
+#include "xfer.hpp"
 namespace tqr {
 
 // dynamic LDS (doubles) of the task paths; the LDS tail (task word, verdicts, ...) follows
@@ -966,6 +1063,8 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
       else
         flow_chain32<B>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                         s_flag);
+    } else if (type == T_UP || type == T_DOWN) {
+      flow_xfer<B, S>(a, type == T_UP, it.m, (it.ts >> 8) & 0xff, s_flag);
     } else {
       flow_panel<B, S>(a, type, it.l, it.k, lds, s_flag);
     }

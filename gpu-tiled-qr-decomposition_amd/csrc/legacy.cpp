@@ -102,13 +102,15 @@ void doCUDADAPP(float* mat) {
   if (st) die("doCUDADAPP", st);
 }
 
+// The reference prints "CPU: x ms" here (qrdecomp.c:219); this call runs on the GPU, so the line
+// says where it ran (the whole call: copies in, factorisation, copies out).
 void taskQRP_threads(float* matData, float* matResult, float* tau, int m, int n, int b, int ldm, int useWY) {
   (void)useWY;
   double t0 = now_ms();
   copy_mat(matData, m, n, ldm, matResult);
   int st = tqr_sgeqrt_host(matResult, tau, m, n, ldm, b);
   if (st) die("taskQRP_threads", st);
-  printf("CPU: %5.2f ms\n", now_ms() - t0);
+  printf("GPU (taskQRP_threads, host pointers, end to end): %5.2f ms\n", now_ms() - t0);
 }
 void taskQRP_threads_d(double* matData, double* matResult, double* tau, int m, int n, int b, int ldm, int useWY) {
   (void)useWY;
@@ -116,7 +118,40 @@ void taskQRP_threads_d(double* matData, double* matResult, double* tau, int m, i
   copy_mat(matData, m, n, ldm, matResult);
   int st = tqr_dgeqrt_host(matResult, tau, m, n, ldm, b);
   if (st) die("taskQRP_threads_d", st);
-  printf("CPU: %5.2f ms\n", now_ms() - t0);
+  printf("GPU (taskQRP_threads_d, host pointers, end to end): %5.2f ms\n", now_ms() - t0);
+}
+
+// The reference's worker-thread loop (qrdecomp.c:306-361, with pthr_getNextTask :242-271 and
+// pthr_doneATask :282-300): a caller that drives its own pthreads over one task grid — each
+// thread runs pthr_doTasks(&info) with a shared ThreadInfo (mutex, condition variable, grid) —
+// gets the same behaviour: under getTaskMutex take the next ready task (bottom-right-first scan,
+// gridscheduler.c:259), waiting on newTasksCond while none is ready; run it (doATask: one tile task
+// on the GPU); register it done and broadcast. Returns (NULL) once the grid reports TASK_DONE —
+// the reference ends with pthread_exit(NULL), the same for a thread start routine.
+void doPthrBcast(pthread_cond_t* cond, int* condMet) {
+  (void)condMet;  // unused by the reference as well (qrdecomp.c:363-367)
+  pthread_cond_broadcast(cond);
+}
+void* pthr_doTasks(void* threadinfoptr) {
+  const ThreadInfo ti = *(const ThreadInfo*)threadinfoptr;
+  int next = TASK_NONE;
+  Task t;
+  while (next != TASK_DONE) {
+    pthread_mutex_lock(ti.getTaskMutex);
+    while ((next = getNextTask(&t, ti.taskGrid, ti.taskM, ti.taskN)) == TASK_NONE)
+      pthread_cond_wait(ti.newTasksCond, ti.getTaskMutex);
+    pthread_mutex_unlock(ti.getTaskMutex);
+    if (next == TASK_AVAIL) {
+      float* ws[2] = {ti.wspace[0], ti.wspace[1]};
+      doATask(t, ti.mat, ti.tau, ti.b, ti.ldm, ws, ti.useWY);
+      pthread_mutex_lock(ti.getTaskMutex);
+      doneATask(ti.taskGrid, ti.taskM, ti.taskN, t);
+      doPthrBcast(ti.newTasksCond, ti.condMet);
+      pthread_mutex_unlock(ti.getTaskMutex);
+    }
+  }
+  doPthrBcast(ti.newTasksCond, ti.condMet);  // release threads still waiting
+  return nullptr;
 }
 
 void doATask(Task t, float* mat, float* tau, int b, int ldm, float** colVect, int useWY) {

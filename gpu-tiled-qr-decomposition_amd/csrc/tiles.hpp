@@ -853,10 +853,17 @@ __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, 
   }
 }
 
+// Work for the waves without panel rows (multi-GPU: forwarding the previous reflector group's
+// images to the peers, flow.hpp panel_idle): step(C) before each reflector step's barrier, fin()
+// after the last one. Defined in flow.hpp.
+struct FwdJob;
+__device__ void panel_idle(const FwdJob* fj, int IB, bool TS);
+
 // PERM: LDS row q of Vs holds tile row vimg_row(q) (the chain engine's paired row order), else
-// tile row q.
+// tile row q. idle: optional work of waves 4-7 (8-wave engine), see FwdJob.
 template <int B, bool TS, bool PERM = false>
-__device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, double* scratch, int c0) {
+__device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, double* scratch, int c0,
+                                          const FwdJob* idle = nullptr) {
   using g = Geo<B>;
   constexpr int IB = g::IB, VP = g::VP, TP = g::TP;
   double* red = scratch;             // 2 x [4 waves][32] cross-wave partials (double-buffered)
@@ -867,7 +874,12 @@ __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, 
   if (t >= 256) {
     // waves beyond the 4 row waves (8-wave engine): no rows, but they would still run the whole
     // VALU reduction stream on zeros and compete with the row waves on their SIMDs — only
-    // match the row waves' barriers (one per reflector step, then the exit ones)
+    // match the row waves' barriers (one per reflector step, then the exit ones), doing the
+    // idle job between them if there is one
+    if (idle) {
+      panel_idle(idle, IB, TS);
+      return;
+    }
     for (int C = 0; C < IB; ++C) __syncthreads();
     __syncthreads();
     if (TS) __syncthreads();

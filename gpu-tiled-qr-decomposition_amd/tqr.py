@@ -253,14 +253,25 @@ def fill_randzo(A, m, n, seed, ldda=None, stream=None):
           "tqr_fill_randzo")
 
 
-def geqrt_host(A, b):
-    """Factorise a host column-major array (shape (n, m)) in place on the GPU; returns the
-    reference's m x n tau matrix (shape (n, m), zero except columns k*b)."""
-    n, m = A.shape
-    tau = np.zeros_like(A)
+def geqrt_host(A, b, with_tau=True, m=None, tau=None):
+    """Factorise a host column-major array (shape (n, ldm)) in place on the GPU; returns the
+    reference's m x n tau matrix (shape (n, ldm), zero except columns k*b; written into `tau` if
+    given, else a new zeroed array), or None with with_tau=False (the reference's cudaQRTask
+    discards tau). m: rows (default ldm)."""
+    n, ldm = A.shape
+    m = m or ldm
+    if with_tau and tau is None:
+        tau = np.zeros_like(A)
+    if with_tau:
+        assert tau.shape == A.shape and tau.dtype == A.dtype and tau.flags.c_contiguous
     fn = lib().tqr_dgeqrt_host if A.dtype == np.float64 else lib().tqr_sgeqrt_host
-    check(fn(_ptr(A), _ptr(tau), m, n, m, b), "tqr_geqrt_host")
+    check(fn(_ptr(A), _ptr(tau) if with_tau else None, m, n, ldm, b), "tqr_geqrt_host")
     return tau
+
+
+def cache_clear():
+    """Release the cached plans and host-API staging buffers (tqr_cache_clear)."""
+    check(lib().tqr_cache_clear(), "tqr_cache_clear")
 
 
 def expand_tau(tau_compact, m, n, b):

@@ -6,13 +6,16 @@
  *
  *   taskQRP_threads (qrdecomp.c:145): copies matData into matResult and factorises it in
  *     place with tile size b; tau receives the m x n tau matrix (ldm), other entries left
- *     untouched as in the reference. Runs on the GPU (no host threads); prints "CPU: x ms"
- *     like the reference, where the time is the whole call. useWY is accepted; both values
- *     compute the same factorisation (the reference's non-WY kernels are dead code).
+ *     untouched as in the reference. Runs on the GPU; where the reference prints "CPU: x ms"
+ *     this prints "GPU (taskQRP_threads, ...): x ms" for the whole call. useWY is accepted; both
+ *     values compute the same factorisation (the reference's non-WY kernels are dead code,
+ *     SURVEY §2 #7).
  *   SGEQRF / SLARFT / STSQRF / SSSRFT (qrdecomp.c:532, 559, 689, 723): one tile task on the
  *     GPU, host pointers, same arguments; m = n = b required (the only way the reference calls
  *     them, qrdecomp.c:395-441); b in {16,32,64,128,256}. Work arrays are ignored.
  *   doATask (qrdecomp.c:377): one DAG task with the reference's tile-pointer contract.
+ *   pthr_doTasks / doPthrBcast (qrdecomp.c:306-367): the reference's worker loop for callers that
+ *     run their own threads over one task grid.
  * D* / *_d: fp64 siblings. Errors print to stderr and abort (no CPU fallback exists).
  * The reference's non-WY kernels (qRSingleBlock ... insSingleHHVector, qrdecomp.c:777-1186)
  * are dead code there (useWY hard-coded to 1, qrdecomp.c:96) and are not provided.
@@ -26,7 +29,14 @@
 extern "C" {
 #endif
 
-struct ThreadInfo { /* qrdecomp.h:6-17, kept for source compatibility */
+/* The reference's worker-thread loop and its broadcast (qrdecomp.h:3-4, qrdecomp.c:306-367): run
+ * pthr_doTasks(&info) on each of your own pthreads, all sharing one ThreadInfo (task grid from
+ * initScheduler, one mutex, one condition variable); every task it takes runs on the GPU through
+ * doATask. Returns NULL when the grid is done. */
+void* pthr_doTasks(void* threadInfo);
+void doPthrBcast(pthread_cond_t* cond, int* condMet);
+
+struct ThreadInfo { /* qrdecomp.h:6-17 (pthr_doTasks' argument) */
     float *mat, *wspace[2], *tau;
     int ldm, b;
     Task* taskGrid;

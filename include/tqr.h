@@ -136,11 +136,28 @@ int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, in
 int tqr_dgeqrt_tiled(int m, int n, int b, double* dA, int ldda, double* dtau_compact, void* stream);
 int tqr_sgeqrt_tiled(int m, int n, int b, float* dA, int ldda, float* dtau_compact, void* stream);
 
-/* Host pointers, blocking: A in place; tau = the reference's m x n tau matrix (ldm). */
+/* Host pointers, blocking: A in place; tau = the reference's m x n tau matrix (ldm), or NULL
+ * (the reference's cudaQRTask discards tau). Any ldm >= m.
+ * With the default (flow) engine the persistent launch moves the matrix itself, overlapping PCIe
+ * with the factorisation: it reads each tile column from host memory just before step 0 needs it
+ * and writes each tile column back as soon as it is final. Host memory is either a pinned staging
+ * buffer that host threads fill and drain while the kernel runs (default), or — environment
+ * TQR_HOST_XFER=register — the caller's array itself, page-locked for the call.
+ * Retention: the plan of each (device, m, n, b, dtype) keeps an m x n device matrix and an
+ * m x kmax tau array, and each device keeps one pinned staging buffer of the largest matrix seen,
+ * until tqr_cache_clear(). Calls on one shape are serialised. */
 int tqr_dgeqrt_host(double* A, double* tau, int m, int n, int ldm, int b);
 int tqr_sgeqrt_host(float* A, float* tau, int m, int n, int ldm, int b);
 /* the same with an explicit engine (tqr_engine) and dtype */
 int tqr_geqrt_host_engine(int dtype, void* A, void* tau, int m, int n, int ldm, int b, int engine);
+/* Release every cached plan of the one-shot helpers (device buffers, pinned buffers) and the
+ * host-API staging buffers; synchronises the device first. Plans created by the caller are not
+ * affected. */
+int tqr_cache_clear(void);
+/* Host-only check of the host-API task list (the flow list plus nxc upload / download tasks per
+ * tile column, a column's upload estimated at tcol chain elements): number of tasks and whether
+ * the estimated-start-time order is topological. */
+int tqr_flow_xfer_plan_check(int M, int N, int b, int seglen, int nxc, double tcol, int* ntasks, int* est_order);
 
 /* Host pointers, single tile tasks on the GPU (the reference's per-tile kernels; used by
  * qrdecomp.h's SGEQRF/SLARFT/STSQRF/SSSRFT and by the per-tile parity tests). Tile pointers

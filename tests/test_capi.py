@@ -83,3 +83,57 @@ def test_flow_plan_export(tqr):
     panels = [it for it in items if (it[0] & 0xff) != 4]
     assert len(panels) == sum(M - k for k in range(min(M, N)))
     assert len(set(items)) == n
+
+
+def test_xfer_plan_topological(tqr):
+    """The host-API task list (flow list + nxc UP / DOWN tasks per tile column, csrc/xfer.hpp):
+    the estimated order is topological for every shape and upload speed, and holds exactly
+    2 * q * nxc transfer tasks more than the device-API list."""
+    import ctypes
+    L = tqr.lib()
+    L.tqr_flow_xfer_plan_check.argtypes = [ctypes.c_int] * 5 + [ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]
+    for M, N, nxc, tcol in ((64, 64, 4, 3.4), (256, 64, 16, 13.6), (8, 12, 1, 0.5), (12, 8, 3, 0.0), (1, 1, 1, 1.0)):
+        nt0, est0 = ctypes.c_int(), ctypes.c_int()
+        assert L.tqr_flow_plan_check(M, N, 256, 8, ctypes.byref(nt0), ctypes.byref(est0)) == 0
+        nt, est = ctypes.c_int(), ctypes.c_int()
+        assert L.tqr_flow_xfer_plan_check(M, N, 256, 8, nxc, tcol, ctypes.byref(nt), ctypes.byref(est)) == 0
+        assert est.value == 1, (M, N)
+        assert nt.value == nt0.value + 2 * N * nxc
+    assert L.tqr_flow_xfer_plan_check(4, 4, 256, 8, 0, 1.0, None, None) == -1
+    assert L.tqr_flow_xfer_plan_check(4, 4, 256, 8, 256, 1.0, None, None) == -1
+
+
+def step_major(items):
+    """A different valid order of a flow list: step by step, panel members first, then the chain
+    segments by column, segment, strip (the engine's always-topological fallback order)."""
+    def key(it):
+        ty = it[0] & 0xff
+        if ty == 4:
+            return (it[3] & 0xffff, 1, it[2], it[3] >> 16, (it[0] >> 8) & 0xff)
+        return (it[3], 0, it[1], 0, 0)
+    return sorted(items, key=key)
+
+
+def test_order_check_accepts_valid_rejects_invalid(tqr):
+    """tqr_flow_order_check (the condition tqr_plan_set_tasks enforces): the exported order and a
+    step-major permutation are accepted; a chain segment moved in front of its panel, or a
+    dropped task, is rejected."""
+    import ctypes
+    L = tqr.lib()
+    M, N, b = 10, 6, 256
+    n = L.tqr_flow_plan_export(M, N, b, 4, None, 0)
+    buf = (ctypes.c_int * (4 * n))()
+    L.tqr_flow_plan_export(M, N, b, 4, buf, n)
+    items = [tuple(buf[4 * x:4 * x + 4]) for x in range(n)]
+
+    def check(lst):
+        arr = (ctypes.c_int * (4 * len(lst)))(*[v for it in lst for v in it])
+        return L.tqr_flow_order_check(M, N, b, arr, len(lst))
+
+    assert check(items) == 1
+    sm = step_major(items)
+    assert sm != items and check(sm) == 1
+    first_chain = next(x for x, it in enumerate(sm) if (it[0] & 0xff) == 4)
+    bad = [sm[first_chain]] + sm[:first_chain] + sm[first_chain + 1:]
+    assert check(bad) == 0
+    assert check(sm[1:]) == 0  # GEQRT(0) missing: everything waits on it

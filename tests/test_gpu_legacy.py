@@ -181,16 +181,51 @@ def test_testDAPP_and_tile_batch(tqr, oracle):
             assert float(np.abs(out[j * b:(j + 1) * b].astype(np.float64) - ref).max()) <= lim
 
 
-def test_compiled_c_driver(tmp_path):
-    """INTEGRATION.md's drop-in: a C program in the shape of the reference's tiledQR, built with
-    gcc against include/ and libtqr.so, prints "Correct."."""
+def _build_driver(tmp_path, name):
     gcc = shutil.which("gcc")
     if gcc is None:
         pytest.skip("no gcc")
-    exe = str(tmp_path / "tiledqr_driver")
+    exe = str(tmp_path / name)
     subprocess.check_call([gcc, "-O2", "-I" + os.path.join(REPO, "include"),
-                           os.path.join(REPO, "tests", "drivers", "tiledqr_driver.c"), "-L" + PKG, "-ltqr",
+                           os.path.join(REPO, "tests", "drivers", name + ".c"), "-L" + PKG, "-ltqr",
                            "-Wl,-rpath," + PKG, "-lpthread", "-lm", "-o", exe])
-    r = subprocess.run([exe, "4"], capture_output=True, text=True, timeout=120)
+    return exe
+
+
+def _driver_outputs(path, m, n, count):
+    raw = np.fromfile(path, dtype=np.float32)
+    assert raw.size == count * m * n
+    return [raw[x * m * n:(x + 1) * m * n].reshape(n, m) for x in range(count)]
+
+
+def test_compiled_c_driver(tmp_path, oracle):
+    """INTEGRATION.md's drop-in: a C program in the shape of the reference's tiledQR, built with
+    gcc against include/ and libtqr.so, prints "Correct." (its GPU runs agree with each other, the
+    reference's own check) — and its outputs match the oracle: taskQRP_threads' matrix and tau and
+    cudaQRTask's matrix, elementwise at the reference's EPSILON 1e-3 (qrdecomp.c:23)."""
+    exe = _build_driver(tmp_path, "tiledqr_driver")
+    out = str(tmp_path / "out.bin")
+    r = subprocess.run([exe, "4", out], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Correct." in r.stdout
+    m = n = 128
+    A, R, T, G = _driver_outputs(out, m, n, 4)
+    F_ref, T_ref = oracle.factor(A, 32)
+    assert np.abs(R - F_ref).max() <= 1e-3 and np.abs(T - T_ref).max() <= 1e-3
+    assert np.abs(G - F_ref).max() <= 1e-3
+
+
+@pytest.mark.parametrize("threads", [1, 2, 4])
+def test_pthr_doTasks_threads(tmp_path, oracle, threads):
+    """The reference's worker loop (pthr_doTasks / doPthrBcast, qrdecomp.c:306-367) driven by the
+    caller's own pthreads over one task grid (tests/drivers/pthr_driver.c, the thread setup of
+    qrdecomp.c:145-230): every task runs on the GPU through doATask; the result matches the oracle
+    (fp32, 1e-3 absolute, qrdecomp.c:23) for 1, 2 and 4 threads."""
+    exe = _build_driver(tmp_path, "pthr_driver")
+    out = str(tmp_path / "out.bin")
+    r = subprocess.run([exe, "4", str(threads), out], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    m = n = 128
+    A, R, T = _driver_outputs(out, m, n, 3)
+    F_ref, T_ref = oracle.factor(A, 32)
+    assert np.abs(R - F_ref).max() <= 1e-3 and np.abs(T - T_ref).max() <= 1e-3

@@ -2,7 +2,9 @@
 list on W workgroups with the kernel's waits (flow.hpp: panel members pipelined per reflector group
 through Rr/Rc/Rt, chain elements waiting per group for the panel images of the NEXT group, Tc for the
 tile's previous step, Ac for the previous segment's head rows) and per-group durations taken from
-the activity stamps (tools/flowstamps.py). Usage: python tools/sched_sim.py [M] [order]"""
+the activity stamps (tools/flowstamps.py). Usage: python tools/sched_sim.py [M]
+Multi-GPU model (tile-column cyclic partition, panel images forwarded to the peers):
+    python tools/sched_sim.py dist [M] [N] [world ...]   -> makespans, S(world), the panel cost S(8) >= 6 needs"""
 import ctypes, heapq, os, sys
 import numpy as np
 
@@ -92,19 +94,6 @@ def simulate(items, M, N, ns=2, prm=P, waits=None):
         busy += end - t0
         heapq.heappush(workers, end)
     return ends.max(), starts, ends
-
-
-if __name__ == "__main__":
-    M = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-    items = export_list(M, M)
-    w = {}
-    span, s, e = simulate(items, M, M, waits=w)
-    print(f"current order: {len(items)} tasks, simulated makespan {span / 1e3:.1f} ms")
-    for c in sorted(w):
-        print(f"  {c:28s} {w[c] / P['W'] / 1e3:7.2f} ms/WG")
-    p0 = dict(P, f=0.0, bt=0.0, t=0.0)
-    span0, _, _ = simulate(items, M, M, prm=p0)
-    print(f"  with free panel compute (PANEL0): {span0 / 1e3:.1f} ms")
 
 
 def tasks_of(M, N, ns=2, seglen=8, seglen_la=None):
@@ -275,3 +264,130 @@ def greedy_order(M, N, ns=2, seglen=8, seglen_la=None, prm=P, prio="panel"):
             if ndep[key(u)] == 0:
                 push(u)
     return order
+
+
+def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="idle", trace=None, pres=0):
+    """The engine on `world` GPUs of W workgroups each: rank r runs the tasks of the global list
+    that it owns (chains of tile column j on j % world, panel k on k % world) in list order. A
+    chain whose panel lives on another rank waits for the member flags instead of Rc: the owner
+    forwards each group's images to the world - 1 peers (fwd_peer us per peer and group) and a
+    flag reaches a peer `hop` us after it is set. mode "inline" (round 2): the panel's 512 threads
+    copy group g's images between its Rc publish and its trailing update (on the member's serial
+    path), flags after its Rt publish; mode "idle" (round 3): waves 4-7 copy group g's images during
+    the factorisation of group g+1 (stretching it only if the copy is longer), flags at its end;
+    the last group inline. pres > 0: each rank reserves `pres` of its W workgroups for panel tasks
+    (a second in-order queue), the others take chain tasks only. Returns the makespan (us)."""
+    NG, W = prm["NG"], prm["W"]
+    fw = fwd_peer * (world - 1)
+    Rr, Rc, E, FL, Tc, G = {}, {}, {}, {}, {}, {}
+    heaps = [[0.0] * (W - pres) for _ in range(world)]
+    pheaps = [[0.0] * pres for _ in range(world)]
+    span = 0.0
+    for (ts, l, m, kk) in items:
+        typ = ts & 0xff
+        if typ != 4:
+            i, k = l, kk
+            r = k % world
+        else:
+            k, j = kk & 0xffff, m
+            r = j % world
+        hp = pheaps[r] if (pres and typ != 4) else heaps[r]
+        t0 = heapq.heappop(hp) + prm["disp"]
+        if typ != 4:
+            t = t0
+            if k > 0:
+                t = max([t] + [Tc[(i, k, s, k - 1)] for s in range(ns)])
+            rr, rc, ee, fl = [0.0] * NG, [0.0] * NG, [0.0] * NG, [0.0] * NG
+            prev = (i - 1, k) if i > k else None
+            for g in range(NG):
+                gs = t if g == 0 else ee[g - 1]
+                if prev:
+                    gs = max(gs, Rr[prev][g])
+                fct = prm["f"]
+                if world > 1 and mode == "idle" and g > 0:
+                    fct = max(fct, fw)  # waves 4-7 copy group g-1 meanwhile
+                rr[g] = gs + prm["io_in"] + fct + prm["io_wb"]
+                rc[g] = rr[g] + prm["bt"] + prm["io_img"]
+                last = g + 1 == NG
+                inline = world > 1 and (mode == "inline" or last)
+                ready = rc[g] + (fw if inline else 0.0)
+                ee[g] = (max(ready, E[prev][g]) if prev else ready) + prm["t"]
+                if world > 1:
+                    if inline:
+                        fl[g] = ee[g] + hop
+                    else:
+                        fl[g - 1] = rr[g] + hop if g > 0 else 0.0
+                if world > 1 and mode == "idle" and g > 0:
+                    fl[g - 1] = rr[g] - prm["io_wb"] + hop
+            Rr[(i, k)], Rc[(i, k)], E[(i, k)], FL[(i, k)] = rr, rc, ee, fl
+            end = ee[-1]
+        else:
+            s = (ts >> 8) & 0xff
+            i0, i1 = l & 0xffff, l >> 16
+            e = kk >> 16
+            remote = world > 1 and (k % world) != r
+            rows = ([k] if e == 0 else []) + list(range(i0, i1))
+            t = t0
+            pg = G[(k, j, s, e - 1)] if e > 0 else None
+            lastg = None
+            for idx, i in enumerate(rows):
+                if k > 0:
+                    t = max(t, Tc[(i, j, s, k - 1)])
+                t += prm["e_ld"]
+                av = FL[(i, k)] if remote else Rc[(i, k)]
+                nxt = (FL if remote else Rc)[(rows[idx + 1], k)][0] if idx + 1 < len(rows) else 0.0
+                g_t = [0.0] * NG
+                for g in range(NG):
+                    need = av[g + 1] if g + 1 < NG else nxt
+                    st = max(t, av[g], need)
+                    if pg is not None and idx == 0:
+                        st = max(st, pg[min(g + 1, NG - 1)])
+                    t = st + prm["c"]
+                    g_t[g] = t
+                t += prm["e_st"]
+                Tc[(i, j, s, k)] = t
+                lastg = g_t
+            G[(k, j, s, e)] = lastg
+            end = t
+        span = max(span, end)
+        heapq.heappush(hp, end)
+        if trace is not None:
+            trace.append((r, t0, end, typ, k))
+    return span
+
+
+def main_dist(argv):
+    M = int(argv[0]) if len(argv) > 0 else 256
+    N = int(argv[1]) if len(argv) > 1 else 64
+    worlds = [int(x) for x in argv[2:]] or [1, 2, 4, 8]
+    items = export_list(M, N)
+    t1 = simulate_dist(items, M, N, 1)
+    print(f"{M}x{N} tiles (b=256): {len(items)} tasks; model makespan on 1 GPU {t1 / 1e3:.1f} ms")
+    for mode in ("inline", "idle"):
+        for w in worlds[1:] if worlds[0] == 1 else worlds:
+            tw = simulate_dist(items, M, N, w, mode=mode)
+            print(f"  {mode:6s} forwarding, {w} GPUs: {tw / 1e3:7.1f} ms  S = {t1 / tw:5.2f}")
+    # the panel cost (factor, T, images, trailing, I/O) scale at which S(8) >= 6 (idle forwarding)
+    for a in (1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 0.4, 0.3):
+        pp = dict(P, f=P["f"] * a, bt=P["bt"] * a, t=P["t"] * a, io_in=P["io_in"] * a, io_wb=P["io_wb"] * a,
+                  io_img=P["io_img"] * a)
+        t8 = simulate_dist(items, M, N, 8, prm=pp)
+        t1a = simulate_dist(items, M, N, 1, prm=pp)
+        cyc = a * (P["f"] + P["bt"] + P["t"] + P["io_in"] + P["io_wb"] + P["io_img"])
+        print(f"  panel group cycle {cyc:5.1f} us: t1 {t1a / 1e3:6.1f} ms, t8 {t8 / 1e3:6.1f} ms, S(8) = {t1a / t8:4.2f}")
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "dist":
+        main_dist(sys.argv[2:])
+    else:
+        M = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+        items = export_list(M, M)
+        w = {}
+        span, s, e = simulate(items, M, M, waits=w)
+        print(f"current order: {len(items)} tasks, simulated makespan {span / 1e3:.1f} ms")
+        for c in sorted(w):
+            print(f"  {c:28s} {w[c] / P['W'] / 1e3:7.2f} ms/WG")
+        p0 = dict(P, f=0.0, bt=0.0, t=0.0)
+        span0, _, _ = simulate(items, M, M, prm=p0)
+        print(f"  with free panel compute (PANEL0): {span0 / 1e3:.1f} ms")
