@@ -114,23 +114,31 @@ struct NoPost32 {
 // MFMAs issued one pair earlier), it is stored (write-through) and the same registers start
 // loading pair p of the next element's strip — the element boundary no longer waits for 128 KiB
 // of strip out and in per workgroup (what-if without strip I/O: -71 ms at 32768^2 fp32).
+// The loads trail the stores by one tile pair: reloading a tile's registers right behind its own
+// store makes the load wait for that store to have read its data (see XPipe in flow.hpp).
 template <int B>
 struct XPipe32 {
+  static constexpr int NMT = Geo32<B>::NMT;
   __amdgpu_buffer_rsrc_t out, in;  // this element's strip / the next element's (same columns)
   unsigned base;
-  __device__ __forceinline__ void xfer(int mt, f4v (&X)[Geo32<B>::NMT]) const {
-    st_f4(out, base + 64u * mt, X[mt]);
-    X[mt] = ld_f4(in, base + 64u * mt);
-  }
-  __device__ __forceinline__ void at(int mt, f4v (&X)[Geo32<B>::NMT]) const {
+  __device__ __forceinline__ void st(int mt, f4v (&X)[NMT]) const { st_f4(out, base + 64u * mt, X[mt]); }
+  __device__ __forceinline__ void ld(int mt, f4v (&X)[NMT]) const { X[mt] = ld_f4(in, base + 64u * mt); }
+  __device__ __forceinline__ void at(int mt, f4v (&X)[NMT]) const {
     if (mt >= 2) {
-      xfer(mt - 2, X);
-      xfer(mt - 1, X);
+      st(mt - 2, X);
+      st(mt - 1, X);
+    }
+    if (mt >= 4) {
+      ld(mt - 4, X);
+      ld(mt - 3, X);
     }
   }
-  __device__ __forceinline__ void fin(f4v (&X)[Geo32<B>::NMT]) const {
-    if constexpr (Geo32<B>::NMT >= 2) xfer(Geo32<B>::NMT - 2, X);
-    xfer(Geo32<B>::NMT - 1, X);
+  __device__ __forceinline__ void fin(f4v (&X)[NMT]) const {
+    if constexpr (NMT >= 2) st(NMT - 2, X);
+    st(NMT - 1, X);
+#pragma unroll
+    for (int mt = NMT - 4; mt < NMT; ++mt)
+      if (mt >= 0) ld(mt, X);
   }
 };
 
@@ -361,12 +369,16 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
           pending = nullptr;
         }
         if (!has_next && g > 0) publish_after_drain(&acg[g - 1], 1);
-        if (t == FLOW_PT) {
-          if (!remote) {
-            pv.prefetch(rc, false);
-          } else {
-            fl_pf = g + 1 < NG ? rf + (size_t)i * NG + g + 1 : has_next ? rf + (size_t)inext * NG : nullptr;
-            fl_pv = fl_pf ? ld_sys(fl_pf) : 0;
+        if (t == FLOW_PT) {  // early load of the counter the next sync point will test
+          const int tg = next_test_group<NG>(g);
+          const bool here = g + 2 < NG;
+          if (here || has_next) {
+            if (!remote) {
+              pv.prefetch(rc, tg, false);
+            } else {
+              fl_pf = rf + (size_t)(here ? i : inext) * NG + tg;
+              fl_pv = ld_sys(fl_pf);
+            }
           }
           if (g + 2 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
         }

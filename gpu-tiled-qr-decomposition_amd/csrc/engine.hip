@@ -65,6 +65,8 @@ __device__ unsigned long long g_pstamps[8];
 __device__ unsigned long long g_fst[4096 * 24];  // >= FST_N categories per workgroup
 __device__ unsigned long long g_ttl[3 << 18];     // task timeline (first 2^18 tasks)
 __device__ unsigned long long g_wst[4096 * 64];   // per-wave activity sums (flow.hpp WSL slots x 8 waves)
+__device__ unsigned long long g_gtr[4096 * 8 * 8];  // group trace of workgroup 0 (flow.hpp GTR)
+__device__ unsigned long long g_xtr[4096 * 8 * 8];  // its hand-over phase-2 marks (flow.hpp XPipe)
 #endif
 }  // namespace tqr
 #include "flow.hpp"
@@ -1592,10 +1594,17 @@ static int geqrt_host_flow(tqr_plan* pl, void* A, void* tau, int ldm, size_t es)
   int* hup = hs->flags;
   int* hdn = hs->flags + q;
   XferArgs xa{dbuf, dbuf, m, hs->dflags, hs->dflags + q, gen};
+  // TQR_HOST_XFER_VERBOSE=1: where the time goes (launch, staging done, kernel, drain done)
+  const bool verbose = getenv("TQR_HOST_XFER_VERBOSE") && atoi(getenv("TQR_HOST_XFER_VERBOSE")) == 1;
+  auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t0 = now();
+  std::atomic<long long> t_up{0}, t_dn{0};
+  if (verbose) HIPCHK(hipEventRecord(pl->ev0, s));
   if ((st = plan_execute_serial(pl, pl->hA, m, pl->hT, s, &xa))) {
     (void)hipStreamSynchronize(s);
     return st;
   }
+  if (verbose) HIPCHK(hipEventRecord(pl->ev1, s));
   // host side, while the launch runs: nu threads stage tile columns in order (the last one to
   // finish a column flags it), nd threads move finished chunks back to the caller's array
   const int nthr = host_threads();
@@ -1612,6 +1621,7 @@ static int geqrt_host_flow(tqr_plan* pl, void* A, void* tau, int ldm, size_t es)
         for (int c = j * b + t; c < (j + 1) * b; c += nu) memcpy(hs->buf + c * col, user + (size_t)c * ldm * es, col);
         if (staged[j].fetch_add(1) + 1 == nu) __atomic_store_n(&hup[j], gen, __ATOMIC_RELEASE);
       }
+      if (verbose) t_up.store(std::max<long long>(t_up.load(), (long long)((now() - t0) * 1e3)));
     });
   for (int t = 0; t < nd; ++t)
     jobs.push_back([&, t] {
@@ -1634,10 +1644,18 @@ static int geqrt_host_flow(tqr_plan* pl, void* A, void* tau, int ldm, size_t es)
         }
         for (int c = j * b + t; c < (j + 1) * b; c += nd) memcpy(user + (size_t)c * ldm * es, hs->buf + c * col, col);
       }
+      if (verbose) t_dn.store(std::max<long long>(t_dn.load(), (long long)((now() - t0) * 1e3)));
     });
   run_jobs(jobs);
   st = tqr_plan_status(pl, s);
   if (st == TQR_OK && failed.load()) st = TQR_EHIP;
+  if (verbose && st == TQR_OK) {
+    float kms = 0;
+    HIPCHK(hipEventElapsedTime(&kms, pl->ev0, pl->ev1));
+    fprintf(stderr, "tqr host xfer: %d host threads (%d in, %d out); staged all columns at %.2f ms, kernel %.2f ms, "
+            "last chunk copied out at %.2f ms, done %.2f ms after the launch call\n", nthr, nu, nd, t_up.load() * 1e-3, kms,
+            t_dn.load() * 1e-3, now() - t0);
+  }
   if (st == TQR_OK && tau) st = tau_out(pl, tau, ldm, es, s);
   return st;
 }
@@ -1918,6 +1936,15 @@ extern "C" int tqr_debug_flow_stamps(unsigned long long* out, int nblocks) {
 extern "C" int tqr_debug_flow_wave_stamps(unsigned long long* out, int nblocks) {
   if (nblocks > 4096) return TQR_EINVAL;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wst), sizeof(unsigned long long) * 8 * WSL * nblocks) != hipSuccess) return TQR_EHIP;
+  return TQR_OK;
+}
+// group trace of workgroup 0 in the last k_flow launch: [group][wave][mark] s_memrealtime (flow.hpp GTR),
+// then the hand-over phase-2 marks [group][wave][8] (XPipe); `out` holds 2 x 64 x ngroups values
+extern "C" int tqr_debug_group_trace(unsigned long long* out, int ngroups) {
+  if (ngroups > GTR_GROUPS) return TQR_EINVAL;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gtr), sizeof(unsigned long long) * 64 * ngroups) != hipSuccess) return TQR_EHIP;
+  if (hipMemcpyFromSymbol(out + 64 * (size_t)ngroups, HIP_SYMBOL(g_xtr), sizeof(unsigned long long) * 64 * ngroups) != hipSuccess)
+    return TQR_EHIP;
   return TQR_OK;
 }
 // task timeline of the last k_flow launch: (start, end, workgroup) per task index, and the task list

@@ -80,17 +80,31 @@ extern __device__ unsigned long long g_wst[];
   } while (0)
 #define WST_MID() const unsigned long long wst1_ = __builtin_amdgcn_s_memrealtime(); WST_ACC(0, wst0_)
 #define WST_END() WST_ACC(1, wst1_)
+// group trace of workgroup 0 (stamps build): per group and wave, the s_memrealtime of marks
+// 0 loop top, 1 before the sync point, 2 after it, 3 phase 1 start, 4 phase 1 end, 5 head I/O end,
+// 6 phase 2 end (tools/group_trace.py)
+constexpr int GTR_GROUPS = 4096;
+extern __device__ unsigned long long g_gtr[];
+extern __device__ unsigned long long g_xtr[];  // [group][wave][8]: XPipe phase-2 progress marks
+#define GTR(mark, tval)                                                                              \
+  do {                                                                                               \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && gtr_n < GTR_GROUPS)                            \
+      g_gtr[((size_t)gtr_n * 8 + (threadIdx.x >> 6)) * 8 + (mark)] = (tval);                         \
+  } while (0)
 #define WMARK_INIT() unsigned long long wt_ = __builtin_amdgcn_s_memrealtime()
 #define WMARK(slot)                     \
   do {                                  \
     WST_ACC(slot, wt_);                 \
     wt_ = __builtin_amdgcn_s_memrealtime(); \
+    GTR(wmark_gtr(slot), wt_);          \
   } while (0)
+__device__ constexpr int wmark_gtr(int slot) { return slot == 7 ? 0 : slot == 2 ? 1 : slot == 3 ? 3 : slot == 4 ? 4 : slot == 5 ? 5 : 6; }
 #else
 #define FST(c) do {} while (0)
 #define WST_T0() do {} while (0)
 #define WMARK_INIT() do {} while (0)
 #define WMARK(slot) do {} while (0)
+#define GTR(mark, tval) do {} while (0)
 #define WST_MID() do {} while (0)
 #define WST_END() do {} while (0)
 #endif
@@ -386,49 +400,54 @@ __device__ __forceinline__ void publish_after_drain(int* p, int delta) {
 
 // The poll thread's view of one panel's group counters Rc[k][0..NG): rv[g] (LDS) holds an
 // observed value, so the V/T images of any member < rv[g] of group g may be LDS-DMA'd.
-// ensure(g, need) re-reads the row (one round trip) only when rv[g] < need. No acquire fence:
+// ensure(g, need) re-reads counter g (one round trip) only when rv[g] < need. No acquire fence:
 // the images are write-once inside a launch (one producer, stored sc1 and drained before its
 // counter add), no workgroup reads a slot before observing its counter, and the DMA itself is
 // an sc1 (L1-bypassing) load — so no CU can hold a stale copy of an image line.
-// prefetch() (the poll thread, right after a sync point) issues the row's loads early, so that
-// the next ensure() normally finds fresh values without an exposed round trip. (Staging the row
-// into LDS by LDS-DMA instead, no registers held: 132.5 ms against 130.6-130.9 at 16384^2.)
+// prefetch(g) (the poll thread, right after a sync point) issues the load of the one counter the
+// next sync point tests, so that ensure() normally finds a fresh value without an exposed round
+// trip. (Round 2 prefetched the whole row into NG registers; in the 256-register budget of the
+// fp64 chain the compiler kept them in scratch, and every reload waited behind the poll wave's
+// outstanding memory operations. Staging the row into LDS by LDS-DMA: 132.5 ms against
+// 130.6-130.9 at 16384^2.)
 template <int NG, int PT = FLOW_PT>
 struct PanelView {
   lds_int_t* rv;
-  int pf[NG];
-  bool pf_valid;
+  int pfv, pfg;  // early-loaded value of counter pfg (-1: none)
   __device__ __forceinline__ void init(int* lds_words) {
     rv = lds_int(lds_words);
-    pf_valid = false;
+    pfg = -1;
+    pfv = 0;
     if (threadIdx.x == PT)
       for (int g = 0; g < NG; ++g) rv[g] = 0;
   }
-  __device__ __forceinline__ void prefetch(int* rc, bool sys) {
-#pragma unroll
-    for (int x = 0; x < NG; ++x) pf[x] = ld_cnt(rc + x, sys);
-    pf_valid = true;
+  __device__ __forceinline__ void prefetch(int* rc, int g, bool sys) {
+    pfv = ld_cnt(rc + g, sys);
+    pfg = g;
   }
   __device__ __forceinline__ bool ensure(int* rc, int g, int need, int* err, bool sys) {
     if (rv[g] >= need) return true;
-    if (pf_valid) {
-#pragma unroll
-      for (int x = 0; x < NG; ++x) rv[x] = max(rv[x], pf[x]);
-      pf_valid = false;
+    if (pfg == g) {
+      rv[g] = max((int)rv[g], pfv);
+      pfg = -1;
       if (rv[g] >= need) return true;
     }
-    int v[NG];
-#pragma unroll
-    for (int x = 0; x < NG; ++x) v[x] = ld_cnt(rc + x, sys);
-#pragma unroll
-    for (int x = 0; x < NG; ++x) rv[x] = v[x];
-    if (rv[g] < need) {
+    const int v = ld_cnt(rc + g, sys);
+    rv[g] = v;
+    if (v < need) {
       if (!spin_ge(rc + g, need, err, sys)) return false;
       rv[g] = ld_cnt(rc + g, sys);
     }
     return true;
   }
 };
+// The group whose counter a chain's next sync point tests, seen from group g's post-sync: group
+// g+2 of this element, or of the next element (group 0 at g = NG-2, group 1 at g = NG-1: the next
+// element's first sync point tests its group 1, its group 0 having been checked before its DMA).
+template <int NG>
+__device__ __forceinline__ int next_test_group(int g) {
+  return g + 2 < NG ? g + 2 : (g + 2 == NG || NG == 1 ? 0 : 1);
+}
 
 // Two consecutive elements (a row pair of a column) as one sc1 buffer access: 16 B for fp64,
 // 8 B for fp32 storage.
@@ -752,22 +771,52 @@ __device__ __forceinline__ void phase_prio(bool phase2) {
 }
 
 // Element hand-over inside the last group's phase 2 (apply_x post hook): once row pair h-1 of the
-// strip is final, it is stored (write-through) and the same registers start loading pair h-1 of
-// the next element's strip — the strip's 512 B per lane out and in ride the MFMA stream instead
-// of sitting between two elements (what-if without strip I/O: -19 ms at 16384^2).
+// strip is final, it is stored (write-through), and the registers of pair h-3 — stored two pairs
+// earlier — start loading pair h-3 of the next element's strip: the strip's 512 B per lane out and
+// in ride the MFMA stream instead of sitting between two elements (what-if without strip I/O:
+// -19 ms at 16384^2). Reloading a pair's registers right behind its own store (round 2) made
+// every load wait for that store to have read its data: the group carrying the hand-over took
+// 40.5 instead of 17.7 us, against 24.2 / 22.4 with the stores / the loads alone (what-if builds,
+// tools/group_trace.py).
 template <int B, typename S>
 struct XPipe {
+#ifndef TQR_XP_LAG
+#define TQR_XP_LAG 2
+#endif
+  static constexpr int NP = Geo<B>::NKS / 2;  // row pairs
+  static constexpr int LAG = TQR_XP_LAG < NP ? TQR_XP_LAG : NP - 1;  // loads trail stores by LAG pairs
   __amdgpu_buffer_rsrc_t out, in;  // this element's strip / the next element's (same columns)
   unsigned base;
-  __device__ __forceinline__ void xfer(int h, double (&X)[Geo<B>::NKS]) const {
-    const unsigned so = base + 8 * h * sizeof(S);
-    st_pair<S, TQR_STRIP_ST_AUX>(out, so, X[2 * h], X[2 * h + 1]);
-    ld_pair<S, TQR_STRIP_LD_AUX>(in, so, X[2 * h], X[2 * h + 1]);
+#ifdef TQR_FLOW_STAMPS
+  unsigned long long* tr;  // (stamps build) progress marks of this phase 2: pairs 0, 8, 16, 24, end
+  __device__ __forceinline__ void mark(int q) const {
+    if (tr && (threadIdx.x & 63) == 0) tr[q] = __builtin_amdgcn_s_memrealtime();
+  }
+#else
+  __device__ __forceinline__ void mark(int) const {}
+#endif
+  __device__ __forceinline__ void st(int h, double (&X)[Geo<B>::NKS]) const {
+#ifndef TQR_DIAG_XP_NOSTORE  // what-if builds (results wrong): the hand-over without its stores / loads
+    st_pair<S, TQR_STRIP_ST_AUX>(out, base + 8 * h * sizeof(S), X[2 * h], X[2 * h + 1]);
+#endif
+  }
+  __device__ __forceinline__ void ld(int h, double (&X)[Geo<B>::NKS]) const {
+#ifndef TQR_DIAG_XP_NOLOAD
+    ld_pair<S, TQR_STRIP_LD_AUX>(in, base + 8 * h * sizeof(S), X[2 * h], X[2 * h + 1]);
+#endif
   }
   __device__ __forceinline__ void at(int h, double (&X)[Geo<B>::NKS]) const {
-    if (h >= 1) xfer(h - 1, X);  // pair h-1 retired one k-step pair ago
+    if (h % 8 == 0) mark(h / 8);
+    if (h >= 1) st(h - 1, X);  // pair h-1 retired one k-step pair ago
+    if (h >= 1 + LAG) ld(h - 1 - LAG, X);
   }
-  __device__ __forceinline__ void fin(double (&X)[Geo<B>::NKS]) const { xfer(Geo<B>::NKS / 2 - 1, X); }
+  __device__ __forceinline__ void fin(double (&X)[Geo<B>::NKS]) const {
+    mark(4);
+    st(NP - 1, X);
+#pragma unroll
+    for (int h = NP - 1 - LAG; h < NP; ++h)
+      if (h >= 0) ld(h, X);
+  }
 };
 
 // Elements: UNMQR(k,j) (segment 0 only, GE-type, the strip of tile (k,j) is X) and TSMQR(i,j,k)
@@ -873,8 +922,17 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     // the register allocator spill ~1 KiB around the poll calls)
     auto groups = [&]() -> bool {
     WMARK_INIT();
+#ifdef TQR_FLOW_STAMPS
+    // (group trace) this wave's running group count, kept in the LDS tail across tasks
+    __attribute__((address_space(3))) int* gtr_c = (__attribute__((address_space(3))) int*)(sflag + 113) + (threadIdx.x >> 6);
+    int gtr_n = *gtr_c;
+#endif
     for (int g = 0; g < NG; ++g) {
+#ifdef TQR_FLOW_STAMPS
+      if ((threadIdx.x & 63) == 0) *gtr_c = gtr_n + 1;
+#endif
       WMARK(7);
+      GTR(7, (unsigned long long)(g | (i << 8) | ((unsigned long long)j << 24) | ((unsigned long long)k << 40)));
       {
         bool ok = true;
 #ifdef TQR_FLOW_STAMPS
@@ -912,6 +970,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
           return false;
 #ifdef TQR_FLOW_STAMPS
         wt_ = __builtin_amdgcn_s_memrealtime();  // (the sync point's own time is in slots 0, 1)
+        GTR(2, wt_);
 #endif
       }
       // (flat read of an LDS word: read here, where little is in flight, as its wait is vmcnt(0))
@@ -925,12 +984,16 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       }
       // segment's last element: its head rows of group g-1 (stored write-through) are drained
       if (!has_next && g > 0) publish_after_drain(&acg[g - 1], 1);
-      if (t == PT) {  // early loads of the counters the next sync point will test
-        if (!remote) {
-          pv.prefetch(rc, false);
-        } else {
-          fl_pf = g + 1 < NG ? rf + (size_t)i * NG + g + 1 : has_next ? rf + (size_t)inext * NG : nullptr;
-          fl_pv = fl_pf ? ld_sys(fl_pf) : 0;
+      if (t == PT) {  // early load of the counter the next sync point will test
+        const int tg = next_test_group<NG>(g);
+        const bool here = g + 2 < NG;  // this element's counter, else the next element's
+        if (here || has_next) {
+          if (!remote) {
+            pv.prefetch(rc, tg, false);
+          } else {
+            fl_pf = rf + (size_t)(here ? i : inext) * NG + tg;
+            fl_pv = ld_sys(fl_pf);
+          }
         }
         if (g + 2 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
       }
@@ -977,7 +1040,11 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         if (pipe) {
           S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
           const XPipe<B, S> xp{uniform_rsrc(Xt + (size_t)col * ldm), uniform_rsrc(Xn + (size_t)col * ldm),
-                               (unsigned)((((size_t)(t & 15)) * ldm + 2 * ((t & 63) >> 4)) * sizeof(S))};
+                               (unsigned)((((size_t)(t & 15)) * ldm + 2 * ((t & 63) >> 4)) * sizeof(S))
+#ifdef TQR_FLOW_STAMPS
+                               , blockIdx.x == 0 && gtr_n < GTR_GROUPS ? g_xtr + ((size_t)gtr_n * 8 + (t >> 6)) * 8 : nullptr
+#endif
+          };
           apply_x4<B, XPipe<B, S>>(Vs, X, W, xp);
         } else {
           apply_x4<B>(Vs, X, W);
@@ -986,6 +1053,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       if (g + 1 == NG) xin = pipe;
       FST(13);
       WMARK(6);
+#ifdef TQR_FLOW_STAMPS
+      ++gtr_n;
+#endif
       if (FLOW_PF) {
 #pragma unroll
         for (int r = 0; r < G::NRI; ++r) H[r] = Hn[r];
@@ -1035,6 +1105,7 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
     for (int c = 0; c < FST_N; ++c) l_[1 + c] = 0;
     unsigned long long* w_ = reinterpret_cast<unsigned long long*>(s_task + 128);
     for (int c = 0; c < 8 * WSL; ++c) w_[c] = 0;
+    for (int c = 0; c < 8; ++c) s_task[114 + c] = 0;  // group-trace counters (flow_chain)
   }
   int* sflag = s_flag;
 #endif

@@ -151,8 +151,12 @@ def _oracle_threads():
 
 def _leading_columns_vs_oracle(oracle, A0, F, tau, m, b, c, tol):
     """Elementwise parity of the leading c columns of a full-size device factorisation with the
-    oracle run on that m x c slice: fp64 max|dF| <= tol * max|F|, |dtau| <= tol * 2; fp32 (tol
-    None) 1e-3 absolute, the reference's EPSILON (qrdecomp.c:23)."""
+    oracle run on that m x c slice: fp64 max|dF| <= tol * max|F|, |dtau| <= tol * 2.
+    fp32 (tol None): the reference's EPSILON (qrdecomp.c:23) is 1e-3 absolute at its own sizes,
+    where |F| stays below ~10; at 32768 rows |R| reaches ~100 and the fp32 oracle's own rounding
+    grows with it, so the bound is 1e-4 relative to max|F| (2e-4 for tau in [1, 2]) — and the GPU's
+    fp32 result must be no farther from the fp64 oracle on the same (fp32) input than the fp32
+    oracle is (the chains run fp32 MFMA, the panels fp64: DESIGN.md §6)."""
     import time
     As = A0[:c].cpu().numpy()
     t0 = time.perf_counter()
@@ -164,7 +168,12 @@ def _leading_columns_vs_oracle(oracle, A0, F, tau, m, b, c, tol):
     dT = max(float(np.abs(Tg[k, k * b:] - T_ref[k * b, k * b:]).max()) for k in range(c // b))
     print(f"leading {c} columns vs oracle: max|dF| = {dF:.3e} (max|F| {np.abs(F_ref).max():.3e}), max|dtau| = {dT:.3e}")
     if tol is None:
-        assert dF <= 1e-3 and dT <= 1e-3
+        assert dF <= 1e-4 * max(1.0, float(np.abs(F_ref).max())) and dT <= 2e-4
+        F64, _ = oracle.factor(As.astype(np.float64), b, threads=_oracle_threads())
+        e_gpu = float(np.abs(Fg - F64).max())
+        e_ref = float(np.abs(F_ref - F64).max())
+        print(f"vs the fp64 oracle: GPU fp32 {e_gpu:.3e}, reference-arithmetic fp32 oracle {e_ref:.3e}")
+        assert e_gpu <= 1.5 * e_ref
     else:
         assert dF <= tol * max(1.0, float(np.abs(F_ref).max()))
         assert dT <= tol * 2
