@@ -342,7 +342,17 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
     const int inext = (i == k) ? i0 : i + 1;
     const bool has_next = inext < i1;
     auto groups = [&]() -> bool {
+#ifdef TQR_FLOW_STAMPS
+      // (group trace, tools/group_trace.py) this wave's running group count in the LDS tail
+      __attribute__((address_space(3))) int* gtr_c = (__attribute__((address_space(3))) int*)(sflag + 113) + (threadIdx.x >> 6);
+      int gtr_n = *gtr_c;
+#endif
       for (int g = 0; g < NG; ++g) {
+#ifdef TQR_FLOW_STAMPS
+        if ((threadIdx.x & 63) == 0) *gtr_c = gtr_n + 1;
+        GTR(0, __builtin_amdgcn_s_memrealtime());
+        GTR(7, (unsigned long long)(g | (i << 8) | ((unsigned long long)j << 24) | ((unsigned long long)k << 40)));
+#endif
         {
           bool ok = true;
           if (t == FLOW_PT && g + 1 == NG) {
@@ -362,7 +372,13 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
             }
           }
           FST(j == k + 1 ? 20 : 0);
+#ifdef TQR_FLOW_STAMPS
+          GTR(1, __builtin_amdgcn_s_memrealtime());
+#endif
           if (!sync_point<true, true>(ok, sflag, par)) return false;
+#ifdef TQR_FLOW_STAMPS
+          GTR(2, __builtin_amdgcn_s_memrealtime());
+#endif
         }
         if (g == 0 && pending) {
           publish_after_drain(pending, 1);
@@ -402,6 +418,9 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
         // per-lane value the two apply32 bodies became exec-masked twins, and at NG == 1 that
         // broke the non-hooked one)
         const bool pipe = NG > 1 && g + 1 == NG && uni(*(volatile int*)(sflag + 44)) != 0;
+#ifdef TQR_FLOW_STAMPS
+        GTR(3, __builtin_amdgcn_s_memrealtime());
+#endif
         if (active) {
           if (ts) {
             // next group's head rows (first element of a later segment) ride this group
@@ -416,6 +435,10 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
               apply32<B, true>(VRp, TPi, X, Hd, dh);
             }
             FST(13);
+#ifdef TQR_FLOW_STAMPS
+            GTR(4, __builtin_amdgcn_s_memrealtime());
+            GTR(5, __builtin_amdgcn_s_memrealtime());
+#endif
             if (!has_next)  // segment's last element: the group's head rows leave (write-through)
 #pragma unroll
               for (int mi = 0; mi < NMI; ++mi) st_f4(hs.rs, hs.off(g * NMI + mi), Hd[mi]);
@@ -437,6 +460,10 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
         }
         if (g + 1 == NG) xin = pipe;
         buf ^= 1;
+#ifdef TQR_FLOW_STAMPS
+        GTR(6, __builtin_amdgcn_s_memrealtime());
+        ++gtr_n;
+#endif
       }
       return true;
     };

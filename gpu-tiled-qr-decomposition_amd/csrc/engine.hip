@@ -438,13 +438,20 @@ static int seglen_la_of(int seglen) {
   const char* esl = getenv("TQR_SEGLEN_LA");
   return esl ? std::max(1, atoi(esl)) : seglen;
 }
+// the last `la_tail` steps (TQR_LA_TAIL): their lookahead column runs one element per segment, so
+// the element that finishes the next diagonal tile runs beside the UNMQR element instead of behind
+// it — the end of the factorisation is a chain of short steps, each waiting for exactly that
+static int la_tail_of() {
+  const char* e = getenv("TQR_LA_TAIL");
+  return e ? std::max(0, atoi(e)) : 0;
+}
 
 static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp, const XferPlan* xp = nullptr) {
   const int kmax = std::min(p, q), ns = (b + FLOW_SW - 1) / FLOW_SW, ng = b / (b < 32 ? b : 32);
   // segment length per chain: shorter segments for the lookahead column pipeline consecutive
   // elements on different workgroups at reflector-group granularity
-  const int seglen_la = seglen_la_of(seglen_);
-  auto seglen_of = [&](int k, int j) { return j == k + 1 ? seglen_la : seglen_; };
+  const int seglen_la = seglen_la_of(seglen_), la_tail = la_tail_of();
+  auto seglen_of = [&](int k, int j) { return seglen_of_chain(k, j, kmax, seglen_, seglen_la, la_tail); };
   // host-pointer API: tile column j arrives (uploaded) at arrive(j); step-0 tasks start after it
   const bool xfer = xp && xp->nxc > 0;
   auto arrive = [&](int j) { return xfer ? (j + 1) * xp->tcol : 0.0; };
@@ -693,7 +700,7 @@ struct tqr_plan {
   // mutex around each enqueue sequence, and every execute's stream waits for the previous one
   std::mutex mu;
   hipEvent_t evDone = nullptr;
-  int seglen = 8, seglen_la = 8;  // chain segment lengths of the flow list (lookahead column: _la)
+  int seglen = 8, seglen_la = 8, la_tail = 0;  // chain segment lengths (flow.hpp seglen_of_chain)
   // host-pointer path (geqrt_host): device matrix and compact tau, kept with the (cached) plan
   // (tqr_cache_clear releases them); hmu serialises whole host-API calls on one plan. The flow
   // engine's transfers run inside its launch (xfer.hpp): a second task list with UP / DOWN
@@ -889,6 +896,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     const char* sl = getenv("TQR_SEGLEN");
     pl->seglen = sl ? std::max(1, atoi(sl)) : 8;
     pl->seglen_la = seglen_la_of(pl->seglen);
+    pl->la_tail = la_tail_of();
     build_flow_plan(pl->p, pl->q, b, pl->seglen, fp);
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
@@ -1227,7 +1235,7 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     f.Rt = f.Ac + (size_t)pl->kmax * pl->q * pl->ns * pl->ng;
     f.Rr = f.Rt + (size_t)pl->kmax * pl->ng;
     f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.peers = pl->d_peers; f.Rf = pl->d_rf;
-    f.seglen = pl->seglen; f.seglen_la = pl->seglen_la;
+    f.seglen = pl->seglen; f.seglen_la = pl->seglen_la; f.la_tail = pl->la_tail;
     if (xa) {
       f.hsrc = xa->hsrc; f.hdst = xa->hdst; f.hld = xa->hld; f.hup = xa->hup; f.hdn = xa->hdn; f.gen = xa->gen;
       f.Uc = f.Rr + (size_t)pl->kmax * pl->ng;

@@ -186,8 +186,15 @@ struct FlowArgs {
   int* hup;
   int* hdn;
   int* Uc;
-  int gen, nxc, xrows, seglen, seglen_la;
+  int gen, nxc, xrows, seglen, seglen_la, la_tail;
 };
+
+// Segment length of chain (k, j): the lookahead column (j = k+1) may use its own (seglen_la), and
+// the last la_tail steps' lookahead column one element per segment (engine.hip la_tail_of).
+__host__ __device__ inline int seglen_of_chain(int k, int j, int kmax, int seglen, int seglen_la, int la_tail) {
+  if (j != k + 1) return seglen;
+  return k >= kmax - la_tail ? 1 : seglen_la;
+}
 
 // ---- synchronisation ---------------------------------------------------------------------
 // Counter accesses go through global (address-space 1) pointers: a generic pointer makes them

@@ -11,9 +11,10 @@ tqr.LIB_PATH = tqr.LIB_PATH.replace("libtqr.so", os.environ.get("TQR_FST_LIB", "
 L = tqr.lib()
 m = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 b = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-A = torch.empty((m, m), dtype=torch.float64, device="cuda")
-tau = torch.zeros((m // b, m), dtype=torch.float64, device="cuda")
-p = tqr.TiledQR(m, m, b, torch.float64)
+dt = torch.float32 if os.environ.get("TQR_FST_DTYPE") == "f32" else torch.float64
+A = torch.empty((m, m), dtype=dt, device="cuda")
+tau = torch.zeros((m // b, m), dtype=dt, device="cuda")
+p = tqr.TiledQR(m, m, b, dt)
 for rep in range(2):
     tqr.fill_randzo(A, m, m, 5)
     p.execute(A, tau)
