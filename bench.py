@@ -74,55 +74,63 @@ def _cpu_model():
     return "unknown"
 
 
-def _cpu_factor(m, n, b, threads):
+def _cpu_factor(m, n, b, threads, f32=False):
     """One full factorisation on the host: the reference's own host path (oracle/_ref, its
-    pthr_doTasks worker loop + gridscheduler.c) when built, else the oracle port. Returns
-    (seconds, kind)."""
+    pthr_doTasks worker loop + gridscheduler.c; fp32 = the unmodified source, fp64 = the same with
+    -Dfloat=double) when built, else the oracle port. Returns (seconds, kind)."""
     import ctypes
 
     import numpy as np
     P = ctypes.c_void_p
-    A = np.zeros((n, m), dtype=np.float64)
+    dt, sfx = (np.float32, "s") if f32 else (np.float64, "d")
+    A = np.zeros((n, m), dtype=dt)
     F = np.zeros_like(A)
     T = np.zeros_like(A)
-    ref = os.path.join(REPO, "oracle", "_ref", "libref_f64_fix.so")
+    ref = os.path.join(REPO, "oracle", "_ref", "libref_f32_fix.so" if f32 else "libref_f64_fix.so")
     if os.path.exists(ref):
         L = ctypes.CDLL(ref)
         L.ref_factor.restype = ctypes.c_double
         L.ref_randzo(A.ctypes.data_as(P), m, n, m, 5)
         return L.ref_factor(A.ctypes.data_as(P), F.ctypes.data_as(P), T.ctypes.data_as(P), m, n, b, m, threads), "reference"
     L = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
-    L.oracle_randzo_d(A.ctypes.data_as(P), m, n, m, 5)
+    getattr(L, f"oracle_randzo_{sfx}")(A.ctypes.data_as(P), m, n, m, 5)
     t0 = time.perf_counter()
-    L.oracle_factor_threads_d(A.ctypes.data_as(P), F.ctypes.data_as(P), T.ctypes.data_as(P), m, n, b, m, threads)
+    getattr(L, f"oracle_factor_threads_{sfx}")(A.ctypes.data_as(P), F.ctypes.data_as(P), T.ctypes.data_as(P), m, n, b, m, threads)
     return time.perf_counter() - t0, "port"
 
 
-def cpu_baseline(sample_n=6144, b=256):
+def cpu_baseline(sample_n=6144, b=256, f32=False, target=(16384, 16384)):
     """the reference host path at 8 threads (qrdecomp.c:21) and at all host cores
-    this process may use. Timed in full: configs[1] (4096^2, b=128) and a 6144^2 b=256 sample of
-    the configs[2] workload; configs[2] itself (16384^2, ~2 min of CPU) is extrapolated from the
-    sample's rate (same tile size, same kernels), and says so."""
+    this process may use. Timed in full: configs[0] (512^2, b=64), configs[1] (4096^2, b=128; fp64
+    only) and a sample^2 b=256 sample of the bench workload (same tile size, same kernels); the
+    workload itself (minutes of CPU) is extrapolated from the sample's rate, and says so. f32: the
+    reference's fp32 build (its native precision) for the fp32 line (configs[4])."""
     nproc = _host_threads()
     legs = {}
     kind = "reference"
+    tm, tn = target
+    prec = "fp32" if f32 else "fp64"
     for name, thr in (("threads_8", 8), ("threads_nproc", nproc)):
         leg = {"threads": thr}
-        t2, kind = _cpu_factor(4096, 4096, 128, thr)
-        leg["c2_4096x4096_b128_s"] = round(t2, 3)
-        leg["c2_gflops"] = round(qr_flops(4096, 4096) / t2 / 1e9, 3)
-        ts, kind = _cpu_factor(sample_n, sample_n, b, thr)
+        t1, kind = _cpu_factor(512, 512, 64, thr, f32)
+        leg["c1_512x512_b64_s"] = round(t1, 4)
+        leg["c1_gflops"] = round(qr_flops(512, 512) / t1 / 1e9, 3)
+        if not f32:
+            t2, kind = _cpu_factor(4096, 4096, 128, thr, f32)
+            leg["c2_4096x4096_b128_s"] = round(t2, 3)
+            leg["c2_gflops"] = round(qr_flops(4096, 4096) / t2 / 1e9, 3)
+        ts, kind = _cpu_factor(sample_n, sample_n, b, thr, f32)
         rate = qr_flops(sample_n, sample_n) / ts
         leg[f"sample_{sample_n}x{sample_n}_b{b}_s"] = round(ts, 3)
         leg["sample_gflops"] = round(rate / 1e9, 3)
-        leg["c3_16384x16384_b256_s_extrapolated"] = round(qr_flops(16384, 16384) / rate, 1)
+        leg[f"target_{tm}x{tn}_b{b}_s_extrapolated"] = round(qr_flops(tm, tn) / rate, 1)
         legs[name] = leg
     t8 = legs["threads_8"]
     return {"value": t8["sample_gflops"], "unit": "GFLOP/s", "cores": 8, "kind": kind,
-            "sample": f"{sample_n}x{sample_n} fp64 b={b} RANDZO seed 5, full factorisation, 8 pthreads "
+            "sample": f"{sample_n}x{sample_n} {prec} b={b} RANDZO seed 5, full factorisation, 8 pthreads "
                       f"(reference taskQRP_threads worker loop, -O2) on {_cpu_model()}",
-            "config": "configs[1] 4096x4096 b=128 timed in full; configs[2] 16384x16384 b=256 extrapolated "
-                      f"from the {sample_n}^2 b={b} sample rate",
+            "config": ("configs[0] 512x512 b=64 timed in full" + ("" if f32 else ", configs[1] 4096x4096 b=128 timed in full")
+                       + f"; the bench workload {tm}x{tn} b={b} extrapolated from the {sample_n}^2 b={b} sample rate"),
             "extrapolated": True,
             "threads_8": legs["threads_8"], "threads_nproc": legs["threads_nproc"]}
 
@@ -400,7 +408,7 @@ def main():
         del Ah, Th
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_sample, 256)
+        cpu = cpu_baseline(args.cpu_sample, 256, f32=args.storage == "f32", target=(m, n))
 
     cfg = 2 if (m, n) == (16384, 16384) else 3 if (m, n) == (65536, 16384) else 1 if (m, n) == (4096, 4096) else "custom"
     if args.storage == "f32":

@@ -16,6 +16,10 @@ cat $OUT/bench.json
 if [ "${FST:-1}" = 1 ] && [ -f gpu-tiled-qr-decomposition_amd/libtqr_fst.so ]; then
   timeout -k 10 120 python tools/flowstamps.py 16384 > $OUT/flowstamps.txt 2>&1 || { echo "flowstamps failed"; tail -20 $OUT/flowstamps.txt; exit 1; }
   grep -v amdgpu.ids $OUT/flowstamps.txt
+  timeout -k 10 120 python tools/timeline.py 16384 > $OUT/timeline.txt 2>&1 || { echo "timeline failed"; tail -20 $OUT/timeline.txt; exit 1; }
+  grep -v amdgpu.ids $OUT/timeline.txt
+  timeout -k 10 120 python tools/group_trace.py 16384 > $OUT/group_trace.txt 2>&1 || { echo "group_trace failed"; tail -20 $OUT/group_trace.txt; exit 1; }
+  grep -v amdgpu.ids $OUT/group_trace.txt
 fi
 if [ "${PROF:-1}" = 1 ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/prof.log; exit 1; }
