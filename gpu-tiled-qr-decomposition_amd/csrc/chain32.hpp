@@ -259,8 +259,8 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
   using G = Geo<B>;
   using G32 = Geo32<B>;
   constexpr int NG = G::NG, NMT = G32::NMT, NMI = G32::NMI, BUF = Img<B, float>::V + Img<B, float>::T;
-  float* A = (float*)a.A;
-  const size_t ldm = a.ldm;
+  float* A = uni((float*)a.A);
+  const size_t ldm = uni64(a.ldm);
   const int t = threadIdx.x, w = t >> 6;
   const int col = s * FLOW_SW + 16 * w;
   const bool active = B % FLOW_SW == 0 || col < B;
@@ -271,26 +271,33 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
   int* const Tc = uni(a.Tc);
   auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B, float>(P, i_, k, g_); };
   auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B, float>(P, i_, k, g_); };
-  int* const rc = &a.Rc[(size_t)k * NG];
-  int* const acg = &a.Ac[(((size_t)k * Q + j) * NS + s) * NG];
+  int* const rc = uni(&a.Rc[(size_t)k * NG]);
+  int* const acg = uni(&a.Ac[(((size_t)k * Q + j) * NS + s) * NG]);
   auto tc = [&](int i) { return &Tc[((size_t)i * Q + j) * NS + s]; };
   f4v X[NMT], Hd[NMT];
   int buf = 0, par = 0;
   int* pending = nullptr;
   bool dma_next = false;
+  // thread 0's early loads as LDS-DMAs into LDS slots (flow.hpp lds_prefetch; every sync point
+  // here drains fully, so each has landed by the next one): the Rc counter (sflag[57]), the Tc of
+  // the next element's tile (sflag[58], -1: none), a remote panel's member flag (sflag[59])
   PanelView<NG> pv;
-  pv.init(sflag + 48);
-  int tc_pf = -1;     // thread 0: Tc of the next element's tile, loaded two groups ahead
+  pv.init(sflag + 48, sflag + 57);
+  int* const tcs = sflag + 58;
+  int* const fls = sflag + 59;
+  if (t == FLOW_PT) {
+    *lds_int(tcs) = -1;
+    *lds_int(fls) = -1;
+  }
   bool xin = false;  // this element's strip was loaded during the previous element's last phase 2
   const bool remote = a.dist && (k % a.world != a.rank);
-  int* const rf = a.Rf + (size_t)k * P * NG;
-  int* fl_pf = nullptr;
-  int fl_pv = 0;
+  int* const rf = uni(a.Rf + (size_t)k * P * NG);
+  int fl_pf = -1;  // index (i * NG + g) of the flag the early load in fls is of
   auto ready = [&](int i_, int g_) -> bool {
     if (!remote) return pv.ensure(rc, g_, i_ - k + 1, err, false);
-    int* fp = rf + (size_t)i_ * NG + g_;
-    if (fp == fl_pf && fl_pv >= 1) return true;
-    return spin_ge(fp, 1, err, true);
+    const int fi = i_ * NG + g_;
+    if (fi == fl_pf && lds_ld_volatile(fls) >= 1) return true;
+    return spin_ge_i(rf + fi, 1, err, true);
   };
   const Strip32<B> hs(At, ldm, col);  // the head tile's strip
   FST(6);
@@ -307,8 +314,8 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
       if (t == FLOW_PT) {
         if (head_in) ok = spin_ge(&acg[0], seg, err);
         FST(9);
-        if (ok && k > 0 && tc_pf < k) ok = spin_ge(tc(i), k, err);
-        tc_pf = -1;
+        if (ok && k > 0 && lds_ld_volatile(tcs) < k) ok = spin_ge(tc(i), k, err);
+        *lds_int(tcs) = -1;
         FST(8);
         if (ok && !dma_next) ok = ready(i, 0);
       }
@@ -361,11 +368,11 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
 #ifdef TQR_DIAG_NOSTRIP
             sflag[44] = 0;
 #else
-            sflag[44] = (NG > 1 && ts && has_next && (k == 0 || tc_pf >= k)) ? 1 : 0;
+            sflag[44] = (NG > 1 && ts && has_next && (k == 0 || lds_ld_volatile(tcs) >= k)) ? 1 : 0;
 #endif
           }
           if (t == FLOW_PT) {
-            if (head_in && g + 1 < NG) ok = spin_ge(&acg[g + 1], seg, err);  // head rows of g+1 final
+            if (head_in && g + 1 < NG) ok = spin_ge_i(&acg[g + 1], seg, err);  // head rows of g+1 final
             if (ok) {
               if (g + 1 < NG) ok = ready(i, g + 1);
               else if (has_next) ok = ready(inext, 0);
@@ -392,11 +399,11 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
             if (!remote) {
               pv.prefetch(rc, tg, false);
             } else {
-              fl_pf = rf + (size_t)(here ? i : inext) * NG + tg;
-              fl_pv = ld_sys(fl_pf);
+              fl_pf = (here ? i : inext) * NG + tg;
+              lds_prefetch<FLOW_PT>(rf + fl_pf, fls, true);
             }
           }
-          if (g + 2 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
+          if (g + 2 == NG && has_next && k > 0) lds_prefetch<FLOW_PT>(tc(inext), tcs, false);
         }
         FST(7);
         const float* img = reinterpret_cast<const float*>(lds + buf * BUF);

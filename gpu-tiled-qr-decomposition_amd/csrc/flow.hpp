@@ -213,6 +213,11 @@ __device__ __forceinline__ int ld_cnt(int* p, bool sys) { return sys ? ld_sys(p)
 // Wave-uniform copies (SGPRs): arguments of a device function arrive in VGPRs, and without a
 // readfirstlane the compiler keeps every value derived from them per lane.
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ size_t uni64(size_t v) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return ((size_t)hi << 32) | lo;
+}
 template <typename T>
 __device__ __forceinline__ T* uni(T* p) {
   const unsigned long long u = (unsigned long long)p;
@@ -222,7 +227,23 @@ __device__ __forceinline__ T* uni(T* p) {
 }
 
 // thread 0 only: spin until *p >= target; false on error / timeout. sys: the counter is written
-// by other devices (system-scope polls)
+// by other devices (system-scope polls). spin_ge_i: the same inlined — the chains' group loops
+// use it, because a call there made the register allocator keep the poll thread's pointers and
+// prefetched counters in scratch (each reload behind an s_waitcnt vmcnt(0), i.e. a full drain of
+// the poll wave's memory operations twice per group).
+__device__ __forceinline__ bool spin_ge_i(int* p, int target, int* err, bool sys = false) {
+  if (ld_cnt(p, sys) >= target) return true;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (ld_cnt(p, sys) < target) {
+    if (ld_relaxed(err)) return false;
+    __builtin_amdgcn_s_sleep(8);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > FLOW_TIMEOUT) {
+      __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+  return true;
+}
 __device__ __noinline__ bool spin_ge(int* p, int target, int* err, bool sys = false) {
   if (ld_cnt(p, sys) >= target) return true;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -417,32 +438,52 @@ __device__ __forceinline__ void publish_after_drain(int* p, int delta) {
 // fp64 chain the compiler kept them in scratch, and every reload waited behind the poll wave's
 // outstanding memory operations. Staging the row into LDS by LDS-DMA: 132.5 ms against
 // 130.6-130.9 at 16384^2.)
+//
+// Round 3: the early load is an LDS-DMA of the one counter word into an LDS slot (lds_prefetch):
+// no VGPR holds it and nothing waits for it. In the VGPR form the value was spilled right after
+// its load (the store to scratch waited for the load — a full round trip on the poll wave after
+// every sync point) and reloaded behind an s_waitcnt vmcnt(0) before the next one.
+typedef __attribute__((address_space(3))) void lds_void_t;
+// Poll thread only (one active lane): start an asynchronous load of *p into the LDS word slot,
+// which reads -1 until it lands. Every chain sync point drains the older memory operations of
+// each wave, so a prefetch issued after one sync point has landed by the next one: the slot is
+// reset (and re-targeted) only after that, and a late write can never land on a newer prefetch.
+template <int PT>
+__device__ __forceinline__ void lds_prefetch(int* p, int* slot, bool sys) {
+  *lds_int(slot) = -1;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the reset is in LDS before the DMA can write
+  // LDS-DMA writes lane-linear (M0 + 4 * lane): aim lane (PT & 63)'s word at the slot
+  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_void_t*)slot - 4u * (PT & 63));
+  if (sys) asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off sc0 sc1" ::"v"(p), "{m0}"(m0) : "memory");
+  else asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, off sc1" ::"v"(p), "{m0}"(m0) : "memory");
+}
 template <int NG, int PT = FLOW_PT>
 struct PanelView {
   lds_int_t* rv;
-  int pfv, pfg;  // early-loaded value of counter pfg (-1: none)
-  __device__ __forceinline__ void init(int* lds_words) {
+  int* pfs;  // LDS slot of the early load (lds_prefetch)
+  int pfg;   // the group whose counter the slot was aimed at (-1: none)
+  __device__ __forceinline__ void init(int* lds_words, int* slot) {
     rv = lds_int(lds_words);
+    pfs = slot;
     pfg = -1;
-    pfv = 0;
     if (threadIdx.x == PT)
       for (int g = 0; g < NG; ++g) rv[g] = 0;
   }
   __device__ __forceinline__ void prefetch(int* rc, int g, bool sys) {
-    pfv = ld_cnt(rc + g, sys);
+    lds_prefetch<PT>(rc + g, pfs, sys);
     pfg = g;
   }
   __device__ __forceinline__ bool ensure(int* rc, int g, int need, int* err, bool sys) {
     if (rv[g] >= need) return true;
     if (pfg == g) {
-      rv[g] = max((int)rv[g], pfv);
+      rv[g] = max((int)rv[g], lds_ld_volatile(pfs));  // (-1 while the load is in flight)
       pfg = -1;
       if (rv[g] >= need) return true;
     }
     const int v = ld_cnt(rc + g, sys);
     rv[g] = v;
     if (v < need) {
-      if (!spin_ge(rc + g, need, err, sys)) return false;
+      if (!spin_ge_i(rc + g, need, err, sys)) return false;
       rv[g] = ld_cnt(rc + g, sys);
     }
     return true;
@@ -842,12 +883,18 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   const int s = uni(s_), i0 = uni(i0_), i1 = uni(i1_), j = uni(j_), k = uni(k_), seg = uni(seg_);
   using G = Geo<B>;
   constexpr int IB = G::IB, NG = G::NG, BUF = G::VIMG + G::TPIMG;
-  S* A = (S*)a.A;
-  const size_t ldm = a.ldm;
+  // (uniform: per-lane copies were spilled, and their reload at every element start waited for
+  // vmcnt(0) — behind the previous element's whole strip hand-over)
+  S* A = uni((S*)a.A);
+  const size_t ldm = uni64(a.ldm);
   const int t = threadIdx.x, w = t >> 6;
   constexpr int PT = FLOW_CHAIN_PT;
   constexpr int HPACK = 2;  // head rows per lane and access (16-B paired head rows, tiles.hpp sigp)
   const int col = s * FLOW_SW + 16 * w;  // this wave's 16 columns inside the tile
+  // byte-free element offset of the wave's first column, made uniform: as a per-lane product the
+  // strip / head base pointers derived from it were VGPR pairs, spilled, and reloaded at every
+  // element start behind an s_waitcnt vmcnt(0) (a full drain of the previous hand-over)
+  const size_t colo = uni64((size_t)col * ldm);
   const bool active = B % FLOW_SW == 0 || col < B;  // (compile-time true unless B < FLOW_SW)
   S* At = A + (size_t)j * B * ldm + (size_t)k * B;  // tile (k,j): the chain's head rows
   // everything the group loop needs from FlowArgs, read once per task: the asm memory clobbers
@@ -859,28 +906,36 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   int* const Tc = uni(a.Tc);
   auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B, S>(P, i_, k, g_); };
   auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B, S>(P, i_, k, g_); };
-  int* const rc = &a.Rc[(size_t)k * NG];
-  int* const acg = &a.Ac[(((size_t)k * Q + j) * NS + s) * NG];  // per head-row group
+  int* const rc = uni(&a.Rc[(size_t)k * NG]);
+  int* const acg = uni(&a.Ac[(((size_t)k * Q + j) * NS + s) * NG]);  // per head-row group
   auto tc = [&](int i) { return &Tc[((size_t)i * Q + j) * NS + s]; };
   double X[G::NKS];
-  double H[G::NRI], Hn[G::NRI], W[G::NRI];
+  double H[G::NRI], W[G::NRI];
   int buf = 0, par = 0;
   int* pending = nullptr;
   bool dma_next = false;  // group 0 of the next element already in flight
+  // poll thread's early loads, LDS-DMA'd into LDS slots (lds_prefetch): the Rc counter the next
+  // sync point tests (sflag[57]), the Tc of the next element's tile, loaded two groups ahead
+  // (sflag[58]; -1: none), the member flag of a remote panel (sflag[59])
   PanelView<NG, PT> pv;
-  pv.init(sflag + 48);
-  int tc_pf = -1;  // poll thread: Tc of the next element's tile, loaded two groups ahead
+  pv.init(sflag + 48, sflag + 57);
+  int* const tcs = sflag + 58;
+  int* const fls = sflag + 59;
+  int* const acs = sflag + 60;  // Ac[g+1] of a later segment's first element, loaded a group ahead
+  if (t == PT) {
+    *lds_int(tcs) = -1;
+    *lds_int(fls) = -1;
+  }
   bool xin = false;  // this element's strip was loaded during the previous element's last phase 2
   // multi-GPU, panel owned by another rank: per-member flags forwarded by the owner
   const bool remote = a.dist && (k % a.world != a.rank);
-  int* const rf = a.Rf + (size_t)k * P * NG;
-  int* fl_pf = nullptr;  // thread 0: the flag the next sync point tests, and its early load
-  int fl_pv = 0;
+  int* const rf = uni(a.Rf + (size_t)k * P * NG);
+  int fl_pf = -1;  // poll thread: index (i * NG + g) of the flag the early load in fls is of
   auto ready = [&](int i_, int g_) -> bool {
     if (!remote) return pv.ensure(rc, g_, i_ - k + 1, err, false);
-    int* fp = rf + (size_t)i_ * NG + g_;
-    if (fp == fl_pf && fl_pv >= 1) return true;
-    return spin_ge(fp, 1, err, true);
+    const int fi = i_ * NG + g_;
+    if (fi == fl_pf && lds_ld_volatile(fls) >= 1) return true;
+    return spin_ge_i(rf + fi, 1, err, true);
   };
   FST(6);
   if (k == 0 && a.Uc) {  // host-pointer API: tile column j uploaded (xfer.hpp)
@@ -895,8 +950,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       if (t == PT) {
         if (i == ifirst && seg > 0) ok = spin_ge(&acg[0], seg, err);
         FST(9);
-        if (ok && k > 0 && tc_pf < k) ok = spin_ge(tc(i), k, err);
-        tc_pf = -1;
+        // (the early load of Tc has landed: a sync point lies between its issue and here)
+        if (ok && k > 0 && lds_ld_volatile(tcs) < k) ok = spin_ge(tc(i), k, err);
+        *lds_int(tcs) = -1;
         FST(8);
         if (ok && !dma_next) ok = ready(i, 0);
       }
@@ -910,18 +966,20 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
     }
     dma_next = false;
-#ifndef TQR_DIAG_NOSTRIP
-    if (active && !xin) load_strip_pair<B, S>(X, Xt, ldm, col);
-#endif
     // head rows: written by another workgroup before this segment or by this one (sc1 loads
     // for both). The UNMQR element (i == k, GE-type V) runs the very same TSMQR code with a zero
     // head: its V image is explicit (zeros above the unit diagonal), so Z = 0 + V^T X and X += V W
     // are exactly the GE update (the zero rows add exact zeros) — one MFMA stream for both
     // element types keeps the register allocation of the hot TSMQR path clean (a separate GE
     // variant with ks0-skipping cost the TSMQR phase 2 its operand prefetch), for ~1 % extra flops.
-    const __amdgpu_buffer_rsrc_t hrs = head_rsrc(At + (size_t)col * ldm, ts);  // UNMQR: empty resource, head = 0
+    // The head rows go first: the compiler moves them into the group loop's registers before the
+    // loop, and that copy waits for them — issued after the strip it waited for the whole strip.
+    const __amdgpu_buffer_rsrc_t hrs = head_rsrc(At + colo, ts);  // UNMQR: empty resource, head = 0
     const unsigned hoff = head_off_pair<B>(ldm, 0);
     if (FLOW_PF && active) load_head_pair<B, TQR_HEAD_LD0_AUX>(H, hrs, hoff);
+#ifndef TQR_DIAG_NOSTRIP
+    if (active && !xin) load_strip_pair<B, S>(X, Xt + colo, ldm, 0);
+#endif
     FST(4);
     const int inext = (i == k) ? i0 : i + 1;
     const bool has_next = inext < i1;
@@ -953,12 +1011,14 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
 #ifdef TQR_DIAG_NOSTRIP
           sflag[44] = 0;
 #else
-          sflag[44] = (NG > 1 && has_next && (k == 0 || tc_pf >= k)) ? 1 : 0;
+          sflag[44] = (NG > 1 && has_next && (k == 0 || lds_ld_volatile(tcs) >= k)) ? 1 : 0;
 #endif
         }
         if (t == PT) {
           // first element of a later segment: head rows of group g+1 (prefetched below) final?
-          if (i == ifirst && seg > 0 && g + 1 < NG) ok = spin_ge(&acg[g + 1], seg, err);
+          // (from group 1 on, its early load sits in acs)
+          if (i == ifirst && seg > 0 && g + 1 < NG && !(g > 0 && lds_ld_volatile(acs) >= seg))
+            ok = spin_ge_i(&acg[g + 1], seg, err);
           if (ok) {
             if (g + 1 < NG) ok = ready(i, g + 1);
             else if (has_next) ok = ready(inext, 0);
@@ -968,8 +1028,10 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         // group 0: the strip / head loads of this element may still be in flight
         constexpr int NX = G::NKS / 2 + (FLOW_PF ? G::NRI / HPACK : 0);
         // full drain where a publish follows: the segment's last element (head rows, Ac) and the
-        // first group after a streamed hand-over (the previous element's strip stores, Tc)
-        const bool full = !has_next || (xin && g == 1);
+        // first group after a streamed hand-over (the previous element's strip stores, Tc); and in
+        // a wave without a strip (B < FLOW_SW): its youngest operations are LDS-DMA instructions of
+        // this group's images, which the counted wait would leave in flight
+        const bool full = !has_next || (xin && g == 1) || !active;
         WMARK(2);
         constexpr int NH = (FLOW_PF ? 2 * G::NRI : G::NRI) / HPACK;  // head stores + next head loads
         if (!(g == 0 ? sync_point_first<NX, PT>(ok, sflag, par, active)
@@ -980,7 +1042,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         GTR(2, wt_);
 #endif
       }
-      // (flat read of an LDS word: read here, where little is in flight, as its wait is vmcnt(0))
+      // (an LDS-typed read: as a flat read its wait was vmcnt(0))
       bool pipe = false;
       if (g + 1 == NG) pipe = *(volatile int*)(sflag + 44) != 0;  // (written before this sync point)
       // the previous element's strip stores are drained: at group 0 (stored before this
@@ -998,11 +1060,12 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
           if (!remote) {
             pv.prefetch(rc, tg, false);
           } else {
-            fl_pf = rf + (size_t)(here ? i : inext) * NG + tg;
-            fl_pv = ld_sys(fl_pf);
+            fl_pf = (here ? i : inext) * NG + tg;
+            lds_prefetch<PT>(rf + fl_pf, fls, true);
           }
         }
-        if (g + 2 == NG && has_next && k > 0) tc_pf = ld_relaxed(tc(inext));
+        if (g + 2 == NG && has_next && k > 0) lds_prefetch<PT>(tc(inext), tcs, false);
+        if (i == ifirst && seg > 0 && g + 2 < NG) lds_prefetch<PT>(&acg[g + 2], acs, false);
       }
       FST(7);
       if (!FLOW_PF && active) load_head_pair<B, 16>(H, hrs, hoff + g * IB * sizeof(S));
@@ -1037,7 +1100,10 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         if (has_next) store_head_pair<B, TQR_HEAD_ST_AUX>(H, hrs, hoff + g * IB * sizeof(S));
         else store_head_pair<B, 16>(H, hrs, hoff + g * IB * sizeof(S));
         FST(2);
-        if (FLOW_PF && g + 1 < NG) load_head_pair<B, TQR_HEAD_LD_AUX>(Hn, hrs, hoff + (g + 1) * IB * sizeof(S));
+        // the next group's head rows straight into H (its stores above have read it): a separate
+        // prefetch register set was copied into H after phase 2, and that copy waited vmcnt(0) —
+        // in the hand-over group for the whole streamed strip
+        if (FLOW_PF && g + 1 < NG) load_head_pair<B, TQR_HEAD_LD_AUX>(H, hrs, hoff + (g + 1) * IB * sizeof(S));
       }
 #endif
       FST(14);
@@ -1046,7 +1112,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       if (active) {
         if (pipe) {
           S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
-          const XPipe<B, S> xp{uniform_rsrc(Xt + (size_t)col * ldm), uniform_rsrc(Xn + (size_t)col * ldm),
+          const XPipe<B, S> xp{uniform_rsrc(Xt + colo), uniform_rsrc(Xn + colo),
                                (unsigned)((((size_t)(t & 15)) * ldm + 2 * ((t & 63) >> 4)) * sizeof(S))
 #ifdef TQR_FLOW_STAMPS
                                , blockIdx.x == 0 && gtr_n < GTR_GROUPS ? g_xtr + ((size_t)gtr_n * 8 + (t >> 6)) * 8 : nullptr
@@ -1063,17 +1129,13 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
 #ifdef TQR_FLOW_STAMPS
       ++gtr_n;
 #endif
-      if (FLOW_PF) {
-#pragma unroll
-        for (int r = 0; r < G::NRI; ++r) H[r] = Hn[r];
-      }
       buf ^= 1;
     }
     return true;
     };
     if (!groups()) return;
 #ifndef TQR_DIAG_NOSTRIP
-    if (active && !xin) store_strip_pair<B, S>(X, Xt, ldm, col);
+    if (active && !xin) store_strip_pair<B, S>(X, Xt + colo, ldm, 0);
 #endif
     pending = tc(i);
     FST(4);
