@@ -12,7 +12,7 @@ OUT=${PMC_OUT:-gpurun_out/pmc}
 mkdir -p $OUT
 run_pass() {  # name, counters...
   local name=$1; shift
-  timeout -s KILL 120 rocprofv3 --pmc "$@" -d $OUT/$name -o pmc --output-format csv -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 ${BENCH_ARGS:-} > $OUT/$name.log 2>&1 || { echo "pmc pass $name failed"; tail -20 $OUT/$name.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc "$@" -d $OUT/$name -o pmc --output-format csv -- python3 bench.py --no-cpu-baseline --no-host-api --steps 1 --warmup 1 ${BENCH_ARGS:-} > $OUT/$name.log 2>&1 || { echo "pmc pass $name failed"; tail -20 $OUT/$name.log; exit 1; }
 }
 run_pass FETCH_SIZE FETCH_SIZE
 run_pass WRITE_SIZE WRITE_SIZE
