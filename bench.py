@@ -178,15 +178,25 @@ def check_owned_columns(A0, A, m, n, b, rank, world):
     return rel
 
 
+def stage_budget(torch, share=1):
+    """Bytes of HBM the bench may spend on staged inputs (one resident copy per timed step): three
+    quarters of what is free on this device, split between the processes sharing it (a one-GPU
+    rehearsal), at most 200 GiB. At 65536 x 16384 fp64 with the driver's 20 steps that is 160 GiB,
+    so both strong-scaling legs time factorisations only."""
+    free, _ = torch.cuda.mem_get_info()
+    return min(200 << 30, int(0.75 * free) // max(1, share))
+
+
 def single_gpu_leg(tqr, torch, m, n, b, dt, steps, warmup):
     """t(1 GPU) of the strong-scaling ratio: the N > 1 workload on this GPU alone, timed like the
-    N-rank leg (staged inputs when steps copies fit in 96 GiB, else a restore inside each step)."""
+    N-rank leg (staged inputs when steps copies fit in stage_budget, else a restore inside each
+    step)."""
     A0 = torch.empty((n, m), dtype=dt, device="cuda")
     tqr.fill_randzo(A0, m, n, 5)
     A = A0.clone()
     tau = torch.zeros((min(m, n) // b, m), dtype=dt, device="cuda")
     plan = tqr.TiledQR(m, n, b, dt)
-    staged = steps * A0.numel() * A0.element_size() <= (96 << 30)
+    staged = steps * A0.numel() * A0.element_size() <= stage_budget(torch)
     As = [A0.clone() for _ in range(steps)] if staged else []
     for _ in range(warmup):
         A.copy_(A0)
@@ -281,7 +291,7 @@ def main():
     # resident copy per timed step is staged before the timed region (the timed region then holds
     # factorisations only); otherwise each step restores its input with a device copy inside it.
     nbytes = A0.numel() * A0.element_size()
-    staged = args.steps * nbytes <= (96 << 30)
+    staged = args.steps * nbytes <= stage_budget(torch, world if rehearsal else 1)
     As = [A0.clone() for _ in range(args.steps)] if staged else []
 
     for _ in range(args.warmup):
