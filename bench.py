@@ -163,10 +163,12 @@ def check_output(A0, A, m, n):
 def check_owned_columns(A0, A, m, n, b, rank, world):
     """The same check for one rank of a multi-GPU factorisation: every column of R lives in its
     tile column, and a tile column is finished by its owner (panel and all its updates), so each
-    rank checks the columns it owns (tile columns j = rank mod world) on its own device."""
+    rank checks the columns it owns (tqr.owned_tile_cols: the snake partition) on its own device."""
     import torch
+    import tqr
     q = n // b
-    cols = torch.arange(n, device=A.device).view(q, b)[rank::world].reshape(-1)
+    own = torch.tensor(tqr.owned_tile_cols(q, rank, world), device=A.device, dtype=torch.long)
+    cols = torch.arange(n, device=A.device).view(q, b)[own].reshape(-1)
     Ao = A[cols].double()  # (n, m) storage: row c = matrix column c
     keep = torch.arange(m, device=A.device)[None, :] <= cols[:, None]  # R: rows r <= c
     nr = torch.linalg.vector_norm(Ao * keep, dim=1)
@@ -279,12 +281,16 @@ def main():
     tau = torch.zeros((min(m, n) // b, m), dtype=dt, device="cuda")
     plan = tqr.TiledQR(m, n, b, dt) if world == 1 else tqr.DistTiledQR(m, n, b, dt)
     stream = torch.cuda.current_stream().cuda_stream
-    # this rank's tile columns (all of them at N = 1): rows j*b..j*b+b-1 of the (n, m) array
-    own_A = A.view(q, b, m)[rank::world]
-    own_A0 = A0.view(q, b, m)[rank::world]
+    # this rank's tile columns (all of them at N = 1; DistTiledQR's snake partition otherwise):
+    # rows j*b..j*b+b-1 of the (n, m) array
+    own_cols = None if world == 1 else torch.tensor(tqr.owned_tile_cols(q, rank, world), device=A.device,
+                                                     dtype=torch.long)
 
     def step():
-        own_A.copy_(own_A0)
+        if own_cols is None:
+            A.copy_(A0)
+        else:
+            A.view(q, b, m)[own_cols] = A0.view(q, b, m)[own_cols]
         plan.execute(A, tau, stream=stream)
 
     # The factorisation is in place, so every timed step needs a fresh input: when HBM allows, one
@@ -355,7 +361,7 @@ def main():
 
     # profiled pass (outside the timed region): per-launch device time of the dominant kernel
     plan.set_profile(True)
-    own_A.copy_(own_A0)
+    A.copy_(A0)
     plan.execute(A, tau, stream=stream)
     torch.cuda.synchronize()
     st = plan.stats()
@@ -424,6 +430,7 @@ def main():
     if args.storage == "f32":
         cfg = 4 if (m, n) == (32768, 32768) else "custom"
     if rank == 0:
+        part = "cyclic" if os.environ.get("TQR_DIST_PART") == "cyclic" else "snake"
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -439,9 +446,9 @@ def main():
             "data": "synthetic (RANDZO distribution, device-generated)",
             "config": {"workload": f"tiled QR {m}x{n} {args.storage} storage, tile {b} (BASELINE configs[{cfg}])", "m": m, "n": n,
                        "tile": b, "parallelism": "single GPU" if world == 1 else
-                       (f"{world} ranks on ONE GPU (rehearsal, TQR_BENCH_DEVICE), tile-column cyclic, panel V/T "
+                       (f"{world} ranks on ONE GPU (rehearsal, TQR_BENCH_DEVICE), tile-column {part}, panel V/T "
                         "forwarded device to device" if rehearsal else
-                        f"{world} GPUs, tile-column cyclic, panel V/T forwarded over xGMI"),
+                        f"{world} GPUs, tile-column {part}, panel V/T forwarded over xGMI"),
                        "inputs": "one resident copy per timed step, staged before the timed region" if staged
                        else "input restored by a device copy inside each timed step"},
             "roofline": roof,

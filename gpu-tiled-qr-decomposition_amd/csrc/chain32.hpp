@@ -290,7 +290,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
     *lds_int(fls) = -1;
   }
   bool xin = false;  // this element's strip was loaded during the previous element's last phase 2
-  const bool remote = a.dist && (k % a.world != a.rank);
+  const bool remote = a.dist && tile_owner(k, a.world, a.cyclic) != a.rank;
   int* const rf = uni(a.Rf + (size_t)k * P * NG);
   int fl_pf = -1;  // index (i * NG + g) of the flag the early load in fls is of
   auto ready = [&](int i_, int g_) -> bool {

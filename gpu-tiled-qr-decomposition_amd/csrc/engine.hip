@@ -589,17 +589,23 @@ static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp, cons
   }
 }
 // Multi-GPU: keep this rank's share of the global (topological) order — panel tasks of the tile
-// columns it owns (column k on rank k % world; each forwards its images to the peers itself) and
+// columns it owns (column k on rank tile_owner(k, world); each forwards its images to the peers itself) and
 // the chain tasks of its own tile columns. Every rank's list is the global order restricted, so
 // the earliest unfinished task of the whole job can always progress: the multi-rank engine is
 // deadlock-free like the single-GPU one.
+// TQR_DIST_PART=cyclic: the round-2 partition j % world (A/B diagnostics; default snake)
+static int dist_cyclic() {
+  const char* e = getenv("TQR_DIST_PART");
+  return e && strcmp(e, "cyclic") == 0;
+}
 static void partition_flow_plan(FlowPlan& fp, int rank, int world) {
+  const int cyc = dist_cyclic();
   std::vector<Item> mine;
   for (const Item& it : fp.items) {
     const int ty = it.ts & 0xff;
     if (ty == T_CHAIN) {
-      if (it.m % world == rank) mine.push_back(it);
-    } else if (it.k % world == rank) {  // QRS(k,k) / QRD(l,k): tile column k
+      if (tile_owner(it.m, world, cyc) == rank) mine.push_back(it);
+    } else if (tile_owner(it.k, world, cyc) == rank) {  // QRS(k,k) / QRD(l,k): tile column k
       mine.push_back(it);
     }
   }
@@ -688,9 +694,9 @@ struct tqr_plan {
   std::vector<int> prof_kind;
   int nl_u = 0, nl_p = 0;
   double ms_u = 0, ms_p = 0;
-  // multi-GPU (tile-column cyclic partition): rank / world, uncached panel counters, forward
-  // counters, peer workspaces opened by IPC
-  int rank = 0, world = 1;
+  // multi-GPU (tile-column snake partition; cyclic = TQR_DIST_PART=cyclic): rank / world, uncached
+  // panel counters, forward counters, peer workspaces opened by IPC
+  int rank = 0, world = 1, cyclic = 0;
   int* d_rf = nullptr;     // multi-GPU member flags (uncached), kmax x p x ng
   PeerBufs* d_peers = nullptr;
   double** d_peer_wk = nullptr;  // world x kmax opened peer workspace pointers
@@ -826,7 +832,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
   tqr_plan* pl = new (std::nothrow) tqr_plan();
   if (!pl) return TQR_ENOMEM;
   pl->m = m; pl->n = n; pl->b = b; pl->p = m / b; pl->q = n / b;
-  pl->rank = rank; pl->world = world;
+  pl->rank = rank; pl->world = world; pl->cyclic = world > 1 && dist_cyclic();
   pl->kmax = std::min(pl->p, pl->q);
   pl->dtype = dtype;
   pl->es = dtype == TQR_F64 ? 8 : 4;
@@ -1081,14 +1087,15 @@ long long tqr_plan_fwd_bytes(const tqr_plan* pl) {
   if (!pl) return TQR_EINVAL;
   if (pl->world < 2) return 0;
   long long members = 0;  // panel members of the tile columns this rank owns
-  for (int k = pl->rank; k < pl->kmax; k += pl->world) members += pl->p - k;
+  for (int k = 0; k < pl->kmax; ++k)
+    if (tile_owner(k, pl->world, pl->cyclic) == pl->rank) members += pl->p - k;
   const long long slot = (long long)(wk_bytes(pl->b, 1, pl->dtype));  // one member's images, all groups
   return members * slot * (pl->world - 1);
 }
 
 int tqr_dist_owner(const tqr_plan* pl, int tile_col) {
   if (!pl || tile_col < 0 || tile_col >= pl->q) return TQR_EINVAL;
-  return tile_col % pl->world;
+  return tile_owner(tile_col, pl->world, pl->cyclic);
 }
 
 int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd) {
@@ -1234,7 +1241,7 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     f.Ac = f.Tc + (size_t)pl->p * pl->q * pl->ns;
     f.Rt = f.Ac + (size_t)pl->kmax * pl->q * pl->ns * pl->ng;
     f.Rr = f.Rt + (size_t)pl->kmax * pl->ng;
-    f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.peers = pl->d_peers; f.Rf = pl->d_rf;
+    f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.cyclic = pl->cyclic; f.peers = pl->d_peers; f.Rf = pl->d_rf;
     f.seglen = pl->seglen; f.seglen_la = pl->seglen_la; f.la_tail = pl->la_tail;
     if (xa) {
       f.hsrc = xa->hsrc; f.hdst = xa->hdst; f.hld = xa->hld; f.hup = xa->hup; f.hdn = xa->hdn; f.gen = xa->gen;

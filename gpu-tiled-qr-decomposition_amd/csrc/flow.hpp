@@ -171,7 +171,7 @@ struct FlowArgs {
   // multi-GPU: dist = world > 1. Rf[k][i][g] (uncached memory) = 1 once the owner of panel k
   // forwarded the V/T images of member i, group g into this rank's workspace (set by the peer
   // over xGMI, polled at system scope). Panel counters Rc/Rr/Rt stay local to the owner.
-  int dist, rank, world;
+  int dist, rank, world, cyclic;  // cyclic: TQR_DIST_PART=cyclic diagnostic partition (j % world)
   const PeerBufs* peers;
   int* Rf;
   // host-pointer API (xfer.hpp; all null / 0 on the device API): the launch uploads its input
@@ -188,6 +188,17 @@ struct FlowArgs {
   int* Uc;
   int gen, nxc, xrows, seglen, seglen_la, la_tail;
 };
+
+// Multi-GPU owner of tile column j (its panel and all its updates): "snake" order over the ranks
+// (0..W-1, W-1..0, 0..W-1, ...), so that every rank's columns sum to the same index total — the
+// chain work of a column grows with its index, and the plain cyclic j % W left the last rank 11 %
+// more work at 65536x16384 on 8 ranks (tools/sched_sim.py dist: S(8) 5.39 vs 5.20).
+// cyclic = 1 (TQR_DIST_PART=cyclic, A/B diagnostics only) restores j % W.
+__host__ __device__ inline int tile_owner(int j, int world, int cyclic = 0) {
+  const int blk = j / world, r = j - blk * world;
+  if (cyclic) return r;
+  return (blk & 1) ? world - 1 - r : r;
+}
 
 // Segment length of chain (k, j): the lookahead column (j = k+1) may use its own (seglen_la), and
 // the last la_tail steps' lookahead column one element per segment (engine.hip la_tail_of).
@@ -928,7 +939,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   }
   bool xin = false;  // this element's strip was loaded during the previous element's last phase 2
   // multi-GPU, panel owned by another rank: per-member flags forwarded by the owner
-  const bool remote = a.dist && (k % a.world != a.rank);
+  const bool remote = a.dist && tile_owner(k, a.world, a.cyclic) != a.rank;
   int* const rf = uni(a.Rf + (size_t)k * P * NG);
   int fl_pf = -1;  // poll thread: index (i * NG + g) of the flag the early load in fls is of
   auto ready = [&](int i_, int g_) -> bool {

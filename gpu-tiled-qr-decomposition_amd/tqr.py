@@ -180,9 +180,25 @@ class TiledQR:
             pass
 
 
+def tile_owner(j, world):
+    """Rank owning tile column j in a multi-GPU factorisation (csrc/flow.hpp tile_owner): snake
+    order over the ranks, 0..W-1 then W-1..0, so every rank's columns sum to the same index total.
+    TQR_DIST_PART=cyclic (read by the library at plan creation too) restores j % W for A/B runs."""
+    blk, r = divmod(j, world)
+    if os.environ.get("TQR_DIST_PART") == "cyclic":
+        return r
+    return world - 1 - r if blk % 2 else r
+
+
+def owned_tile_cols(q, rank, world):
+    """The tile columns 0..q-1 that `rank` owns."""
+    return [j for j in range(q) if tile_owner(j, world) == rank]
+
+
 class DistTiledQR(TiledQR):
     """One rank's share of a multi-GPU factorisation (tile-column cyclic partition, one process
-    per GPU; include/tqr.h "multi-GPU"). Tile column j belongs to rank j % world. The handle
+    per GPU; include/tqr.h "multi-GPU"). Tile column j belongs to rank tile_owner(j, world) (snake
+    order 0..W-1, W-1..0, ...). The handle
     exchange and the per-factorisation barrier go over torch.distributed (`group`); the panel
     data moves GPU to GPU inside the persistent launch (xGMI stores into IPC-opened peer
     workspaces), not through the collective library."""
@@ -220,7 +236,7 @@ class DistTiledQR(TiledQR):
             say("ready")
 
     def owns(self, tile_col):
-        return tile_col % self.world == self.rank
+        return tile_owner(tile_col, self.world) == self.rank
 
     def fwd_bytes(self):
         """Bytes this rank forwards to its peers per factorisation (panel V/T images over xGMI)."""

@@ -106,9 +106,11 @@ int tqr_plan_stats(const tqr_plan* plan, int* nlaunch_update, double* ms_update,
 /* Number of flat-tree tasks (reference calcTotalTasks, src/gpucalc.cu:1546, for all m,n). */
 long tqr_total_tasks(int m, int n, int b);
 
-/* ---- multi-GPU: tile-column cyclic partition, one process per GPU ------------------------
- * Rank r owns tile columns j with j % world == r and factors them in a full-size matrix of
- * its own (only its columns are valid at the end; tau column k lives on rank k % world). The
+/* ---- multi-GPU: tile-column partition, one process per GPU ---------------------------------
+ * Rank r owns the tile columns j with tqr_dist_owner(j) == r — snake order over the ranks
+ * (0..W-1, W-1..0, 0..W-1, ...: every rank's columns sum to the same index total, balancing the
+ * chain work that grows with j) — and factors them in a full-size matrix of
+ * its own (only its columns are valid at the end; tau column k lives on the owner of column k). The
  * owner of panel k forwards each finished reflector group's V/T images to every peer over
  * xGMI inside the persistent launch (peer workspaces opened by IPC), so panels of successive
  * steps overlap across GPUs exactly as on one GPU. Sequence per factorisation, every rank:

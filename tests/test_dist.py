@@ -41,7 +41,7 @@ def test_partition_covers_global_list(M, N):
             nt, nf = tqr.dist_plan_check(M, N, b, r, world)
             tasks += nt
             fwd += nf
-            own_panel = sum(M - k for k in range(kmax) if k % world == r)
+            own_panel = sum(M - k for k in range(kmax) if tqr.tile_owner(k, world) == r)
             assert nf == own_panel
         assert fwd == npanel
         assert tasks == total  # panel tasks forward their own images: no extra tasks

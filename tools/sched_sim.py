@@ -266,9 +266,20 @@ def greedy_order(M, N, ns=2, seglen=8, seglen_la=None, prm=P, prio="panel"):
     return order
 
 
-def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="idle", trace=None, pres=0):
+def owner_of(j, world, kind="cyclic"):
+    """rank owning tile column j: snake (0..W-1, W-1..0, ...: every rank's columns sum to the same
+    index total, balancing the chain work that grows with j; the engine's partition since round 3)
+    or cyclic (j % world, rounds 1-2)."""
+    if kind == "snake":
+        blk, r = divmod(j, world)
+        return r if blk % 2 == 0 else world - 1 - r
+    return j % world
+
+
+def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="idle", trace=None, pres=0,
+                  part="snake"):
     """The engine on `world` GPUs of W workgroups each: rank r runs the tasks of the global list
-    that it owns (chains of tile column j on j % world, panel k on k % world) in list order. A
+    that it owns (chains of tile column j and panel j on owner_of(j)) in list order. A
     chain whose panel lives on another rank waits for the member flags instead of Rc: the owner
     forwards each group's images to the world - 1 peers (fwd_peer us per peer and group) and a
     flag reaches a peer `hop` us after it is set. mode "inline" (round 2): the panel's 512 threads
@@ -287,10 +298,10 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
         typ = ts & 0xff
         if typ != 4:
             i, k = l, kk
-            r = k % world
+            r = owner_of(k, world, part)
         else:
             k, j = kk & 0xffff, m
-            r = j % world
+            r = owner_of(j, world, part)
         hp = pheaps[r] if (pres and typ != 4) else heaps[r]
         t0 = heapq.heappop(hp) + prm["disp"]
         if typ != 4:
@@ -325,7 +336,7 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
             s = (ts >> 8) & 0xff
             i0, i1 = l & 0xffff, l >> 16
             e = kk >> 16
-            remote = world > 1 and (k % world) != r
+            remote = world > 1 and owner_of(k, world, part) != r
             rows = ([k] if e == 0 else []) + list(range(i0, i1))
             t = t0
             pg = G[(k, j, s, e - 1)] if e > 0 else None
