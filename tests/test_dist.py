@@ -1,4 +1,4 @@
-"""Multi-GPU path (tile-column cyclic partition).
+"""Multi-GPU path (tile-column snake partition).
 
 CPU (no GPU): every rank's task list is the global list restricted to its tile columns plus
 one forward task per owned panel member — checked for world sizes 1-8 and inside a world-2
@@ -45,6 +45,27 @@ def test_partition_covers_global_list(M, N):
             assert nf == own_panel
         assert fwd == npanel
         assert tasks == total  # panel tasks forward their own images: no extra tasks
+
+
+@pytest.mark.parametrize("q,world", [(64, 8), (64, 4), (16, 2), (24, 8)])
+def test_snake_partition_balances_column_work(q, world):
+    """Every rank owns q/world tile columns whose indices sum to the same total (the chain work of
+    column j grows with j); the round-2 cyclic j % world gave the last rank the most."""
+    cols = [tqr.owned_tile_cols(q, r, world) for r in range(world)]
+    assert sorted(c for cs in cols for c in cs) == list(range(q))
+    assert {len(cs) for cs in cols} == {q // world}
+    if (q // world) % 2 == 0:
+        assert len({sum(cs) for cs in cols}) == 1
+
+
+def test_cyclic_partition_knob(monkeypatch):
+    """TQR_DIST_PART=cyclic (A/B diagnostics) switches the library and tqr.tile_owner together."""
+    monkeypatch.setenv("TQR_DIST_PART", "cyclic")
+    M, N, world = 16, 8, 4
+    for r in range(world):
+        assert tqr.owned_tile_cols(N, r, world) == list(range(r, N, world))
+        _, nf = tqr.dist_plan_check(M, N, 256, r, world)
+        assert nf == sum(M - k for k in range(N) if k % world == r)
 
 
 def _gloo_worker(rank, world, port, q):
