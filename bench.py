@@ -9,12 +9,14 @@ qrdecomp.c:1383). A step = restore the input from a resident HBM copy (device-to
 included in the step) + one whole factorisation. GFLOP/s uses the algorithmic count
 2mn^2 - 2n^3/3.
 
-N > 1 (torchrun, one process per GPU): ONE matrix, BASELINE.json configs[3] by default
-(65536 x 16384 fp64, tile 256), factorised by all ranks together — tile column j on rank
-j % N, the owner of each panel forwarding its reflector groups' V/T images to the peers over
-xGMI inside the persistent launch (DESIGN.md §7). Total work is fixed ("scaling": "strong");
-value = the matrix's algorithmic flops / max-over-ranks time. Each step restores the rank's
-own tile columns from a resident copy, resets its counters, barriers, and factorises.
+N > 1 (one process per GPU): ONE matrix, BASELINE.json configs[3] by default
+(65536 x 16384 fp64, tile 256), factorised by all ranks together — tile columns dealt to the
+ranks in snake order, the owner of each panel forwarding its reflector groups' V/T images to the
+peers over xGMI inside the persistent launch. Total work is fixed ("scaling":
+"strong"); value = the matrix's algorithmic flops / max-over-ranks time. A plain
+`python bench.py --gpus N` starts the N ranks itself (torch.distributed.run as a child process,
+before anything touches the GPU; launch_plan / spawn_ranks); under an external launcher
+(WORLD_SIZE set) --gpus must agree with it.
 
 Extra objects on the line:
   roofline      — the dominant kernel (trailing-update: TSMQR/UNMQR strips on
@@ -160,14 +162,17 @@ def check_output(A0, A, m, n):
     return rel
 
 
-def check_owned_columns(A0, A, m, n, b, rank, world):
+def check_owned_columns(A0, A, m, n, b, rank, world, owned=None):
     """The same check for one rank of a multi-GPU factorisation: every column of R lives in its
     tile column, and a tile column is finished by its owner (panel and all its updates), so each
-    rank checks the columns it owns (tqr.owned_tile_cols: the snake partition) on its own device."""
+    rank checks the columns it owns on its own device. owned: those tile columns as the plan deals
+    them (DistTiledQR.owned_cols); default the snake partition (tqr.owned_tile_cols)."""
     import torch
     import tqr
     q = n // b
-    own = torch.tensor(tqr.owned_tile_cols(q, rank, world), device=A.device, dtype=torch.long)
+    if owned is None:
+        owned = tqr.owned_tile_cols(q, rank, world)
+    own = torch.tensor(owned, device=A.device, dtype=torch.long)
     cols = torch.arange(n, device=A.device).view(q, b)[own].reshape(-1)
     Ao = A[cols].double()  # (n, m) storage: row c = matrix column c
     keep = torch.arange(m, device=A.device)[None, :] <= cols[:, None]  # R: rows r <= c
@@ -222,7 +227,79 @@ def single_gpu_leg(tqr, torch, m, n, b, dt, steps, warmup):
             "t1_column_norm_rel_err": rel}
 
 
+def launch_plan(gpus, env, ndev):
+    """How `bench.py --gpus N` runs: ("run", None) in this process (N = 1, or already one rank of an
+    external torch.distributed.run), ("spawn", None) = start N ranks as a child launcher, or
+    ("error", message). ndev: visible devices (a callable, so that it is only asked when needed;
+    torch.cuda.device_count() does not initialise the GPU). TQR_BENCH_DEVICE pins every rank to one
+    device (a one-GPU rehearsal), so the device count does not bound N then."""
+    if gpus < 1:
+        return "error", f"--gpus {gpus}: must be >= 1"
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "error", f"--gpus {gpus} disagrees with WORLD_SIZE={ws} set by the launcher"
+        return "run", None
+    if gpus == 1:
+        return "run", None
+    if "TQR_BENCH_DEVICE" not in env:
+        have = ndev()
+        if gpus > have:
+            return "error", f"--gpus {gpus} but only {have} device(s) are visible"
+    return "spawn", None
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(gpus, argv, popen=None):
+    """Run this script as `gpus` ranks under torch.distributed.run, as a CHILD process (nothing here
+    has touched the GPU, and no exec replaces this process). The child's stdout is relayed line by
+    line: the rank-0 JSON line to our stdout, everything else to stderr. Returns the exit code to
+    use: the child's, or 1 if it exited 0 without printing a JSON line."""
+    import subprocess
+    popen = popen or subprocess.Popen
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    print(f"bench: launching {gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    child = popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    got = False
+    for ln in child.stdout:
+        s = ln.strip()
+        if s.startswith("{") and '"metric"' in s:
+            print(s, flush=True)
+            got = True
+        else:
+            print(ln.rstrip("\n"), file=sys.stderr, flush=True)
+    rc = child.wait()
+    if rc == 0 and not got:
+        print("bench: the ranks exited without a result line", file=sys.stderr, flush=True)
+        return 1
+    return rc
+
+
 def main():
+    # (before any torch / GPU call: N > 1 without an external launcher starts the ranks as a child)
+    gi = None
+    for x, a in enumerate(sys.argv[1:]):
+        if a == "--gpus" and x + 2 < len(sys.argv):
+            gi = sys.argv[x + 2]
+        elif a.startswith("--gpus="):
+            gi = a.split("=", 1)[1]
+    if gi is not None:
+        def ndev():
+            import torch
+            return torch.cuda.device_count()
+        how, msg = launch_plan(int(gi), os.environ, ndev)
+        if how == "error":
+            print(f"bench: {msg}", file=sys.stderr, flush=True)
+            sys.exit(2)
+        if how == "spawn":
+            sys.exit(spawn_ranks(int(gi), sys.argv[1:]))
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -283,8 +360,7 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     # this rank's tile columns (all of them at N = 1; DistTiledQR's snake partition otherwise):
     # rows j*b..j*b+b-1 of the (n, m) array
-    own_cols = None if world == 1 else torch.tensor(tqr.owned_tile_cols(q, rank, world), device=A.device,
-                                                     dtype=torch.long)
+    own_cols = None if world == 1 else torch.tensor(plan.owned_cols(), device=A.device, dtype=torch.long)
 
     def step():
         if own_cols is None:
@@ -300,10 +376,26 @@ def main():
     staged = args.steps * nbytes <= stage_budget(torch, world if rehearsal else 1)
     As = [A0.clone() for _ in range(args.steps)] if staged else []
 
+    # N > 1: an engine error (a cross-device wait that timed out, error word set, workgroups drained)
+    # or a failed column check on one rank is recorded in that rank's `status` and reported in the
+    # line (value null, exit code 1) instead of raising on one rank while the others wait
+    rank_status = "ok"
+
+    def engine_status(where):
+        nonlocal rank_status
+        if not dist:
+            plan.status(stream)
+            return
+        try:
+            plan.status(stream)
+        except tqr.TQRError as e:
+            if rank_status == "ok":
+                rank_status = f"{where}: {e}"
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    plan.status(stream)  # the engine's error word (outside the timed region)
+    engine_status("warmup")  # the engine's error word (outside the timed region)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -322,15 +414,24 @@ def main():
         tt = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
-    plan.status(stream)
+    engine_status("timed steps")
     Afin = As[-1] if staged and args.steps else A  # the last timed step's output
-    ok_rel = check_output(A0, Afin, m, n) if world == 1 else check_owned_columns(A0, Afin, m, n, b, rank, world)
+    if world == 1:
+        ok_rel = check_output(A0, Afin, m, n)
+    else:
+        try:
+            ok_rel = check_owned_columns(A0, Afin, m, n, b, rank, world, plan.owned_cols())
+        except RuntimeError as e:
+            ok_rel = None
+            if rank_status == "ok":
+                rank_status = f"check: {e}"
     del As, Afin
     dist_info = None
+    failed = []
     if dist:
-        # per rank: engine status (raised above if not ok), forwarded bytes, and with a stamps build
+        # per rank: engine status, forwarded bytes, and with a stamps build
         # (TQR_LIB=libtqr_fst.so) the share of workgroup time the panels spent forwarding
-        mine = {"rank": rank, "status": "ok", "fwd_bytes": plan.fwd_bytes(), "column_norm_rel_err": ok_rel}
+        mine = {"rank": rank, "status": rank_status, "fwd_bytes": plan.fwd_bytes(), "column_norm_rel_err": ok_rel}
         L = tqr.lib()
         if hasattr(L, "tqr_debug_flow_stamps"):
             import ctypes
@@ -346,7 +447,19 @@ def main():
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
         dist_info = {"world_size": world, "ranks": ranks}
+        failed = [r["rank"] for r in ranks if r["status"] != "ok"]
     ms_step = el / args.steps * 1e3
+    if failed:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps,
+                              "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+                              "scaling": "strong", "vs_baseline": None, "dtype": args.storage,
+                              "error": f"rank(s) {failed} failed (see dist.ranks[*].status)",
+                              "config": {"workload": f"tiled QR {m}x{n} {args.storage} storage, tile {b}", "m": m,
+                                         "n": n, "tile": b},
+                              "dist": dist_info}), flush=True)
+        dist.destroy_process_group()
+        sys.exit(1)
     strong = None
     if single:
         strong = dict(single, tN_ms=round(ms_step, 3), tN_inputs="staged" if staged else "restored in step",

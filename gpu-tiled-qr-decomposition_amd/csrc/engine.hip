@@ -432,40 +432,56 @@ struct XferPlan {
   double tcol = 0.0;
 };
 
-// chain segment length of the lookahead column (j = k+1, the DAG's critical path: its chain
-// elements feed the next panel's members): TQR_SEGLEN_LA, else the plan's seglen
-static int seglen_la_of(int seglen) {
+// Order knobs of the flow task list, read from the environment ONCE per plan (plan_create) and
+// kept with it: the host-API task list (plan_xfer_list, built at the first host call) and the
+// device's column-final counts (xfer.hpp, from FlowArgs) must see the same segment lengths as the
+// plan's own list, whatever the environment says later.
+//   seglen     chain segment length (TQR_SEGLEN, default 8)
+//   seglen_la  the lookahead column's (j = k+1, the DAG's critical path: its chain elements feed
+//              the next panel's members; TQR_SEGLEN_LA, default seglen)
+//   la_tail    the last la_tail steps (TQR_LA_TAIL): their lookahead column runs one element per
+//              segment, so the element that finishes the next diagonal tile runs beside the UNMQR
+//              element instead of behind it
+//   Tg         the estimator's panel group-step cost in chain elements (TQR_TG, default 1.4)
+//   lazy       TQR_LAZY (default 1), la / lac: TQR_LA / TQR_LAC (see build_flow_plan)
+struct FlowKnobs {
+  int seglen = 8, seglen_la = 8, la_tail = 0;
+  double Tg = 1.4, lazy = 1.0, la = 0.0, lac = 0.0;
+};
+static FlowKnobs knobs_from_env(int seglen) {
+  FlowKnobs kn;
+  kn.seglen = std::max(1, seglen);
   const char* esl = getenv("TQR_SEGLEN_LA");
-  return esl ? std::max(1, atoi(esl)) : seglen;
-}
-// the last `la_tail` steps (TQR_LA_TAIL): their lookahead column runs one element per segment, so
-// the element that finishes the next diagonal tile runs beside the UNMQR element instead of behind
-// it — the end of the factorisation is a chain of short steps, each waiting for exactly that
-static int la_tail_of() {
+  kn.seglen_la = esl ? std::max(1, atoi(esl)) : kn.seglen;
   const char* e = getenv("TQR_LA_TAIL");
-  return e ? std::max(0, atoi(e)) : 0;
+  kn.la_tail = e ? std::max(0, atoi(e)) : 0;
+  if (const char* eg = getenv("TQR_TG")) kn.Tg = atof(eg);
+  if (const char* el = getenv("TQR_LAZY")) kn.lazy = atof(el);
+  if (const char* ela = getenv("TQR_LA")) kn.la = atof(ela);
+  kn.lac = kn.la;
+  if (const char* elac = getenv("TQR_LAC")) kn.lac = atof(elac);  // lookahead column's chains (default: TQR_LA)
+  return kn;
+}
+static int env_seglen() {
+  const char* sl = getenv("TQR_SEGLEN");
+  return sl ? std::max(1, atoi(sl)) : 8;
 }
 
-static void build_flow_plan(int p, int q, int b, int seglen_, FlowPlan& fp, const XferPlan* xp = nullptr) {
+static void build_flow_plan(int p, int q, int b, const FlowKnobs& kn, FlowPlan& fp, const XferPlan* xp = nullptr) {
   const int kmax = std::min(p, q), ns = (b + FLOW_SW - 1) / FLOW_SW, ng = b / (b < 32 ? b : 32);
   // segment length per chain: shorter segments for the lookahead column pipeline consecutive
   // elements on different workgroups at reflector-group granularity
-  const int seglen_la = seglen_la_of(seglen_), la_tail = la_tail_of();
-  auto seglen_of = [&](int k, int j) { return seglen_of_chain(k, j, kmax, seglen_, seglen_la, la_tail); };
+  auto seglen_of = [&](int k, int j) { return seglen_of_chain(k, j, kmax, kn.seglen, kn.seglen_la, kn.la_tail); };
   // host-pointer API: tile column j arrives (uploaded) at arrive(j); step-0 tasks start after it
   const bool xfer = xp && xp->nxc > 0;
   auto arrive = [&](int j) { return xfer ? (j + 1) * xp->tcol : 0.0; };
   // cost model (unit: one chain element): Tg = one panel group-step; tunable for experiments
-  const char* eg = getenv("TQR_TG");
-  const double Tg = eg ? atof(eg) : 1.4, Te = 1.0;
-  const char* el = getenv("TQR_LAZY");
-  const double lazy = el ? atof(el) : 1.0;
+  const double Tg = kn.Tg, Te = 1.0;
+  const double lazy = kn.lazy;
   // lookahead (TQR_LA / TQR_LAC, unit: chain elements): panel tasks / the lookahead column's
   // chains are keyed this much earlier than their estimate (the critical path first)
-  const char* ela = getenv("TQR_LA");
-  const double la = ela ? atof(ela) : 0.0;
-  const char* elac = getenv("TQR_LAC");  // lookahead column's chains (default: TQR_LA)
-  const double lac = elac ? atof(elac) : la;
+  const double la = kn.la;
+  const double lac = kn.lac;
   // fin_elem[k][i][j] (strips move together in the estimate): finish of chain element (i,j,k)
   auto id3 = [&](int k, int i, int j) { return ((size_t)k * p + i) * q + j; };
   std::vector<double> fin((size_t)kmax * p * q, 0.0), pstart((size_t)kmax * p, 0.0);
@@ -706,13 +722,14 @@ struct tqr_plan {
   // mutex around each enqueue sequence, and every execute's stream waits for the previous one
   std::mutex mu;
   hipEvent_t evDone = nullptr;
-  int seglen = 8, seglen_la = 8, la_tail = 0;  // chain segment lengths (flow.hpp seglen_of_chain)
+  FlowKnobs knobs;  // task-list order knobs, read once at creation (segment lengths: flow.hpp seglen_of_chain)
   // host-pointer path (geqrt_host): device matrix and compact tau, kept with the (cached) plan
   // (tqr_cache_clear releases them); hmu serialises whole host-API calls on one plan. The flow
   // engine's transfers run inside its launch (xfer.hpp): a second task list with UP / DOWN
   // tasks (d_flow_x), nxc chunks of xrows rows per tile column. The wave engine stages through
   // two pinned buffers (pin, pev, sC) before / after its launches.
   std::mutex hmu;
+  std::atomic<int> users{0};  // one-shot helpers using this cached plan right now (PlanRef)
   void* hA = nullptr;
   void* hT = nullptr;
   Item* d_flow_x = nullptr;
@@ -899,16 +916,13 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
   pl->ng = b / ib;
   if (pl->engine == TQR_ENGINE_FLOW) {
     FlowPlan fp;
-    const char* sl = getenv("TQR_SEGLEN");
-    pl->seglen = sl ? std::max(1, atoi(sl)) : 8;
-    pl->seglen_la = seglen_la_of(pl->seglen);
-    pl->la_tail = la_tail_of();
-    build_flow_plan(pl->p, pl->q, b, pl->seglen, fp);
+    pl->knobs = knobs_from_env(env_seglen());
+    build_flow_plan(pl->p, pl->q, b, pl->knobs, fp);
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
-    // next, err, Rc, Tc, Ac, Rt, Rr, then Uc (upload chunks per tile column, host-pointer API)
-    pl->sync_ints = 2 + 3 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns +
+    // next, err, wait limit (ms, flow.hpp timed_out), Rc, Tc, Ac, Rt, Rr, then Uc (upload chunks per tile column, host-pointer API)
+    pl->sync_ints = 3 + 3 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns +
                     (size_t)pl->kmax * pl->q * pl->ns * pl->ng + (size_t)pl->q;
     if (pl->nflow <= 0 || hipMalloc(&pl->d_flow, sizeof(Item) * pl->nflow) != hipSuccess ||
         hipMalloc(&pl->d_sync, sizeof(int) * pl->sync_ints) != hipSuccess ||
@@ -1101,7 +1115,7 @@ int tqr_dist_owner(const tqr_plan* pl, int tile_col) {
 int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1 || world < 1 || rank < 0 || rank >= world) return TQR_EINVAL;
   FlowPlan fp;
-  build_flow_plan(M, N, b, seglen, fp);
+  build_flow_plan(M, N, b, knobs_from_env(seglen), fp);
   if (world > 1) partition_flow_plan(fp, rank, world);
   if (ntasks) *ntasks = (int)fp.items.size();
   if (nfwd) {  // panel members that forward their images (the panel tasks, when world > 1)
@@ -1150,7 +1164,7 @@ int tqr_plan_debug_workspace(const tqr_plan* pl, int k, void* host, size_t bytes
 int tqr_flow_plan_export(int M, int N, int b, int seglen, int* items, int cap) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1) return TQR_EINVAL;
   FlowPlan fp;
-  build_flow_plan(M, N, b, seglen, fp);
+  build_flow_plan(M, N, b, knobs_from_env(seglen), fp);
   const int n = (int)fp.items.size();
   if (items)
     for (int x = 0; x < n && x < cap; ++x) {
@@ -1163,7 +1177,7 @@ int tqr_flow_plan_export(int M, int N, int b, int seglen, int* items, int cap) {
 int tqr_flow_plan_check(int M, int N, int b, int seglen, int* ntasks, int* est_order) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1) return TQR_EINVAL;
   FlowPlan fp;
-  build_flow_plan(M, N, b, seglen, fp);
+  build_flow_plan(M, N, b, knobs_from_env(seglen), fp);
   if (ntasks) *ntasks = (int)fp.items.size();
   if (est_order) *est_order = fp.est_order;
   return TQR_OK;
@@ -1175,7 +1189,7 @@ int tqr_flow_xfer_plan_check(int M, int N, int b, int seglen, int nxc, double tc
   XferPlan xp;
   xp.nxc = nxc;
   xp.tcol = tcol;
-  build_flow_plan(M, N, b, seglen, fp, &xp);
+  build_flow_plan(M, N, b, knobs_from_env(seglen), fp, &xp);
   if (ntasks) *ntasks = (int)fp.items.size();
   if (est_order) *est_order = fp.est_order;
   return TQR_OK;
@@ -1206,6 +1220,13 @@ int tqr_plan_stats(const tqr_plan* pl, int* nu, double* msu, int* np, double* ms
 }
 
 static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_t cs, const XferArgs* xa = nullptr);
+// Wait limit of a host-pointer launch (flow.hpp timed_out): 5 s plus the matrix at 200 MB/s — the
+// host stages the input column by column while the launch runs, at whatever rate it gets (one
+// host thread, a busy host); the 5 s limit of device-resident launches would call that an error.
+static int host_wait_ms(const tqr_plan* pl) {
+  const double bytes = (double)pl->es * pl->m * pl->n;
+  return (int)std::min(2.0e9, 5000.0 + bytes / 200e3);
+}
 // Serialised enqueue of one execute (see tqr.h): the stream first waits for the plan's previous
 // execute; evDone marks this one. If enqueuing fails part-way, evDone is still recorded behind
 // whatever was enqueued (the wave engine's side streams are joined first), so the next execute
@@ -1236,13 +1257,13 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     f.tasks = xa ? pl->d_flow_x : pl->d_flow;
     f.ntasks = xa ? pl->nflow_x : pl->nflow;
     f.m = pl->m; f.p = pl->p; f.q = pl->q; f.kmax = pl->kmax; f.ns = pl->ns;
-    f.next = pl->d_sync; f.err = pl->d_sync + 1; f.Rc = pl->d_sync + 2;
+    f.next = pl->d_sync; f.err = pl->d_sync + 1; f.Rc = pl->d_sync + 3;
     f.Tc = f.Rc + (size_t)pl->kmax * pl->ng;
     f.Ac = f.Tc + (size_t)pl->p * pl->q * pl->ns;
     f.Rt = f.Ac + (size_t)pl->kmax * pl->q * pl->ns * pl->ng;
     f.Rr = f.Rt + (size_t)pl->kmax * pl->ng;
     f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.cyclic = pl->cyclic; f.peers = pl->d_peers; f.Rf = pl->d_rf;
-    f.seglen = pl->seglen; f.seglen_la = pl->seglen_la; f.la_tail = pl->la_tail;
+    f.seglen = pl->knobs.seglen; f.seglen_la = pl->knobs.seglen_la; f.la_tail = pl->knobs.la_tail;
     if (xa) {
       f.hsrc = xa->hsrc; f.hdst = xa->hdst; f.hld = xa->hld; f.hup = xa->hup; f.hdn = xa->hdn; f.gen = xa->gen;
       f.Uc = f.Rr + (size_t)pl->kmax * pl->ng;
@@ -1253,6 +1274,8 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     }
     // multi-GPU: counters and flags are reset by tqr_dist_reset (all ranks, then a barrier)
     if (pl->world == 1) HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
+    // host-pointer API: every wait may depend on the host staging the input (see timed_out)
+    if (xa) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(pl->d_sync + 2), host_wait_ms(pl), 1, cs));
     if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
     hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(FLOW_NT), pl->ldsF, cs, f);
     HIPCHK(hipGetLastError());
@@ -1326,27 +1349,46 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
 static std::mutex g_cache_mu;
 static std::map<std::tuple<int, int, int, int, int, int>, tqr_plan*> g_cache;
 
-static int cached_plan(int m, int n, int b, int dtype, tqr_plan** out, int engine = TQR_ENGINE_DEFAULT) {
+// A cached plan in use by a one-shot helper: counted in plan->users from the lookup (under
+// g_cache_mu) until the call returns, so tqr_cache_clear never frees a plan another thread is
+// still using (it unlinks the plans first, then waits for each one's users to drain).
+struct PlanRef {
+  tqr_plan* pl = nullptr;
+  PlanRef() = default;
+  PlanRef(const PlanRef&) = delete;
+  PlanRef& operator=(const PlanRef&) = delete;
+  ~PlanRef() {
+    if (pl) pl->users.fetch_sub(1);
+  }
+};
+static int cached_plan(int m, int n, int b, int dtype, PlanRef& ref, int engine = TQR_ENGINE_DEFAULT) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return TQR_ENODEV;
   std::lock_guard<std::mutex> lk(g_cache_mu);
   auto key = std::make_tuple(dev, m, n, b, dtype, engine);
   auto itc = g_cache.find(key);
-  if (itc != g_cache.end()) { *out = itc->second; return TQR_OK; }
-  int st = tqr_plan_create_engine(out, m, n, b, dtype, engine);
-  if (st == TQR_OK) g_cache[key] = *out;
-  return st;
+  tqr_plan* pl = nullptr;
+  if (itc != g_cache.end()) {
+    pl = itc->second;
+  } else {
+    int st = tqr_plan_create_engine(&pl, m, n, b, dtype, engine);
+    if (st) return st;
+    g_cache[key] = pl;
+  }
+  pl->users.fetch_add(1);
+  ref.pl = pl;
+  return TQR_OK;
 }
 
 int tqr_dgeqrt_tiled(int m, int n, int b, double* dA, int ldda, double* dtau, void* stream) {
-  tqr_plan* pl;
-  int st = cached_plan(m, n, b, TQR_F64, &pl);
-  return st ? st : tqr_plan_execute(pl, dA, ldda, dtau, stream);
+  PlanRef r;
+  int st = cached_plan(m, n, b, TQR_F64, r);
+  return st ? st : tqr_plan_execute(r.pl, dA, ldda, dtau, stream);
 }
 int tqr_sgeqrt_tiled(int m, int n, int b, float* dA, int ldda, float* dtau, void* stream) {
-  tqr_plan* pl;
-  int st = cached_plan(m, n, b, TQR_F32, &pl);
-  return st ? st : tqr_plan_execute(pl, dA, ldda, dtau, stream);
+  PlanRef r;
+  int st = cached_plan(m, n, b, TQR_F32, r);
+  return st ? st : tqr_plan_execute(r.pl, dA, ldda, dtau, stream);
 }
 
 // Host-pointer factorisation (the reference's calling convention: cudaQRTask copies a host matrix
@@ -1537,7 +1579,7 @@ static int plan_xfer_list(tqr_plan* pl) {
   const double elem_s = 4.0 * pl->b * pl->b * FLOW_SW / (pl->dtype == TQR_F64 ? 0.175e12 : 0.38e12);
   xp.tcol = ((double)pl->m * pl->b * pl->es / (gbs * 1e9)) / elem_s;
   FlowPlan fp;
-  build_flow_plan(pl->p, pl->q, pl->b, pl->seglen, fp, &xp);
+  build_flow_plan(pl->p, pl->q, pl->b, pl->knobs, fp, &xp);  // the plan's own knobs (not the environment now)
   Item* d = nullptr;
   if (hipMalloc(&d, sizeof(Item) * fp.items.size()) != hipSuccess) return TQR_ENOMEM;
   if (hipMemcpy(d, fp.items.data(), sizeof(Item) * fp.items.size(), hipMemcpyHostToDevice) != hipSuccess) {
@@ -1630,9 +1672,13 @@ static int geqrt_host_flow(tqr_plan* pl, void* A, void* tau, int ldm, size_t es)
   for (auto& x : staged) x.store(0);
   std::atomic<int> failed{0};
   std::vector<std::function<void()>> jobs;
+  // TQR_HOST_STAGE_DELAY_MS (tests only): a slow host, each tile column staged that much later
+  const char* edl = getenv("TQR_HOST_STAGE_DELAY_MS");
+  const int stage_delay_ms = edl ? std::max(0, atoi(edl)) : 0;
   for (int t = 0; t < nu; ++t)
     jobs.push_back([&, t] {
       for (int j = 0; j < q; ++j) {
+        if (stage_delay_ms) std::this_thread::sleep_for(std::chrono::milliseconds(stage_delay_ms));
         for (int c = j * b + t; c < (j + 1) * b; c += nu) memcpy(hs->buf + c * col, user + (size_t)c * ldm * es, col);
         if (staged[j].fetch_add(1) + 1 == nu) __atomic_store_n(&hup[j], gen, __ATOMIC_RELEASE);
       }
@@ -1677,9 +1723,10 @@ static int geqrt_host_flow(tqr_plan* pl, void* A, void* tau, int ldm, size_t es)
 
 static int geqrt_host(void* A, void* tau, int m, int n, int ldm, int b, int dtype, int engine = TQR_ENGINE_DEFAULT) {
   if (!A || ldm < m || !valid_b(b) || m <= 0 || n <= 0 || m % b || n % b) return TQR_EINVAL;
-  tqr_plan* pl;
-  int st = cached_plan(m, n, b, dtype, &pl, engine);
+  PlanRef ref;
+  int st = cached_plan(m, n, b, dtype, ref, engine);
   if (st) return st;
+  tqr_plan* pl = ref.pl;
   std::lock_guard<std::mutex> lk(pl->hmu);
   const size_t es = dtype == TQR_F64 ? 8 : 4;
   if (pl->engine == TQR_ENGINE_FLOW) return geqrt_host_flow(pl, A, tau, ldm, es);
@@ -1702,21 +1749,37 @@ int tqr_geqrt_host_engine(int dtype, void* A, void* tau, int m, int n, int ldm, 
 }
 
 // Release every cached plan (the one-shot helpers' and the host API's device matrices, compact
-// tau, pinned buffers) and the host-API staging buffers. Waits for the device first.
+// tau, pinned buffers) and the host-API staging buffers. Safe against concurrent tqr calls: the
+// plans are unlinked from the cache under its lock (later calls build new ones), then each is
+// destroyed once no call still uses it (PlanRef count) and its last execute has finished (its
+// evDone event, whatever device or stream it ran on). A staging buffer is released under its own
+// mutex, which a host-API call holds from before its launch until its last copy out; the
+// HostStage objects themselves are kept (a call may hold a pointer to one), so a later call just
+// allocates again.
 int tqr_cache_clear(void) {
-  if (hipDeviceSynchronize() != hipSuccess) return TQR_EHIP;
-  std::lock_guard<std::mutex> lk(g_cache_mu);
-  for (auto& kv : g_cache) tqr_plan_destroy(kv.second);
-  g_cache.clear();
-  for (auto& kv : g_stage) {
-    {
-      std::lock_guard<std::mutex> l2(kv.second->mu);
-      kv.second->release();
-    }
-    delete kv.second;
+  std::vector<tqr_plan*> plans;
+  std::vector<HostStage*> stages;
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    for (auto& kv : g_cache) plans.push_back(kv.second);
+    g_cache.clear();
+    for (auto& kv : g_stage) stages.push_back(kv.second);
   }
-  g_stage.clear();
-  return TQR_OK;
+  int st = TQR_OK;
+  for (tqr_plan* pl : plans) {
+    while (pl->users.load() > 0) std::this_thread::yield();
+    {
+      std::lock_guard<std::mutex> l1(pl->hmu);
+      std::lock_guard<std::mutex> l2(pl->mu);
+      if (pl->evDone && hipEventSynchronize(pl->evDone) != hipSuccess) st = TQR_EHIP;
+    }
+    tqr_plan_destroy(pl);
+  }
+  for (HostStage* hs : stages) {
+    std::lock_guard<std::mutex> l2(hs->mu);
+    hs->release();
+  }
+  return st;
 }
 
 int tqr_fill_randzo(int dtype, void* dA, int m, int n, int ldda, unsigned long long seed, void* stream) {

@@ -102,15 +102,16 @@ void doCUDADAPP(float* mat) {
   if (st) die("doCUDADAPP", st);
 }
 
-// The reference prints "CPU: x ms" here (qrdecomp.c:219); this call runs on the GPU, so the line
-// says where it ran (the whole call: copies in, factorisation, copies out).
+// The reference prints "CPU: %5.2f ms" here (qrdecomp.c:219). The line keeps that prefix (callers
+// and scripts parse it) and says after the number where it ran: the whole call, copies in,
+// factorisation on the GPU, copies out.
 void taskQRP_threads(float* matData, float* matResult, float* tau, int m, int n, int b, int ldm, int useWY) {
   (void)useWY;
   double t0 = now_ms();
   copy_mat(matData, m, n, ldm, matResult);
   int st = tqr_sgeqrt_host(matResult, tau, m, n, ldm, b);
   if (st) die("taskQRP_threads", st);
-  printf("GPU (taskQRP_threads, host pointers, end to end): %5.2f ms\n", now_ms() - t0);
+  printf("CPU: %5.2f ms (taskQRP_threads on the GPU, host pointers, end to end)\n", now_ms() - t0);
 }
 void taskQRP_threads_d(double* matData, double* matResult, double* tau, int m, int n, int b, int ldm, int useWY) {
   (void)useWY;
@@ -118,7 +119,7 @@ void taskQRP_threads_d(double* matData, double* matResult, double* tau, int m, i
   copy_mat(matData, m, n, ldm, matResult);
   int st = tqr_dgeqrt_host(matResult, tau, m, n, ldm, b);
   if (st) die("taskQRP_threads_d", st);
-  printf("GPU (taskQRP_threads_d, host pointers, end to end): %5.2f ms\n", now_ms() - t0);
+  printf("CPU: %5.2f ms (taskQRP_threads_d on the GPU, host pointers, end to end)\n", now_ms() - t0);
 }
 
 // The reference's worker-thread loop (qrdecomp.c:306-361, with pthr_getNextTask :242-271 and

@@ -82,6 +82,7 @@ def lib():
     L.tqr_dist_import.argtypes = [_P, ctypes.c_char_p, ctypes.c_size_t]
     L.tqr_dist_reset.argtypes = [_P, _P]
     L.tqr_plan_status.argtypes = [_P, _P]
+    L.tqr_dist_owner.argtypes = [_P, _I]
     L.tqr_dgeqrt_host.argtypes = [_P, _P, _I, _I, _I, _I]
     L.tqr_sgeqrt_host.argtypes = [_P, _P, _I, _I, _I, _I]
     _lib = L
@@ -183,7 +184,8 @@ class TiledQR:
 def tile_owner(j, world):
     """Rank owning tile column j in a multi-GPU factorisation (csrc/flow.hpp tile_owner): snake
     order over the ranks, 0..W-1 then W-1..0, so every rank's columns sum to the same index total.
-    TQR_DIST_PART=cyclic (read by the library at plan creation too) restores j % W for A/B runs."""
+    TQR_DIST_PART=cyclic restores j % W for A/B runs. Host-only helper (tests, planning): code that
+    holds a plan asks the plan (DistTiledQR.owner), which read TQR_DIST_PART once, at creation."""
     blk, r = divmod(j, world)
     if os.environ.get("TQR_DIST_PART") == "cyclic":
         return r
@@ -233,10 +235,31 @@ class DistTiledQR(TiledQR):
             allb = b"".join(blocks)
             say("import")
             check(lib().tqr_dist_import(self.h, allb, len(allb)), "tqr_dist_import")
+            # every rank must deal the tile columns the same way (TQR_DIST_PART is read per process
+            # at plan creation): a disagreement would deadlock the launch, so fail here instead
+            mine = self.owners()
+            every = [None] * self.world
+            dist.all_gather_object(every, mine, group=group)
+            if any(o != mine for o in every):
+                raise TQRError("DistTiledQR: ranks disagree on the tile-column partition (TQR_DIST_PART)")
             say("ready")
 
+    def owner(self, tile_col):
+        """Rank owning tile column tile_col, as this plan partitions (tqr_dist_owner)."""
+        r = lib().tqr_dist_owner(self.h, tile_col)
+        if r < 0:
+            check(r, "tqr_dist_owner")
+        return r
+
+    def owners(self):
+        return [self.owner(j) for j in range(self.n // self.b)]
+
+    def owned_cols(self):
+        """The tile columns this rank owns (its panels and all their updates)."""
+        return [j for j, r in enumerate(self.owners()) if r == self.rank]
+
     def owns(self, tile_col):
-        return tile_owner(tile_col, self.world) == self.rank
+        return self.owner(tile_col) == self.rank
 
     def fwd_bytes(self):
         """Bytes this rank forwards to its peers per factorisation (panel V/T images over xGMI)."""

@@ -47,3 +47,65 @@ def test_check_owned_columns_sees_only_its_columns():
     A[b + 3, 7] -= 1.0
     A[b + 3, 200] += 1.0  # below the diagonal (V): not part of R
     assert bench.check_owned_columns(A0, A, m, n, b, 1, 2) < 1e-12
+
+
+# ---- bench.py --gpus N launch decision (a plain `bench.py --gpus N` must start N ranks) ----
+def _ndev(n):
+    def f():
+        return n
+    return f
+
+
+def test_launch_plan_decisions():
+    assert bench.launch_plan(1, {}, _ndev(8)) == ("run", None)
+    assert bench.launch_plan(8, {}, _ndev(8)) == ("spawn", None)
+    how, msg = bench.launch_plan(8, {}, _ndev(4))
+    assert how == "error" and "only 4" in msg
+    # one-GPU rehearsal: every rank pinned to one device, the device count does not bound N
+    assert bench.launch_plan(4, {"TQR_BENCH_DEVICE": "0"}, _ndev(1)) == ("spawn", None)
+    # under an external launcher: run as one of its ranks, and --gpus must agree with it
+    assert bench.launch_plan(2, {"WORLD_SIZE": "2"}, _ndev(0)) == ("run", None)
+    how, msg = bench.launch_plan(4, {"WORLD_SIZE": "2"}, _ndev(8))
+    assert how == "error" and "WORLD_SIZE" in msg
+    assert bench.launch_plan(0, {}, _ndev(8))[0] == "error"
+
+
+def test_launch_plan_does_not_count_devices_unless_needed():
+    def boom():
+        raise AssertionError("device count asked")
+    assert bench.launch_plan(1, {}, boom) == ("run", None)
+    assert bench.launch_plan(2, {"WORLD_SIZE": "2"}, boom) == ("run", None)
+    assert bench.launch_plan(2, {"TQR_BENCH_DEVICE": "0"}, boom) == ("spawn", None)
+
+
+class _FakeChild:
+    def __init__(self, lines, rc):
+        self.stdout = iter(lines)
+        self._rc = rc
+
+    def wait(self):
+        return self._rc
+
+
+def test_spawn_ranks_relays_json_and_exit_code(capsys):
+    seen = {}
+
+    def popen(cmd, **kw):
+        seen["cmd"] = cmd
+        return _FakeChild(["noise from a rank\n", '{"metric": "m", "value": 1.0, "n_gpus": 2}\n'], 0)
+
+    rc = bench.spawn_ranks(2, ["--gpus", "2", "--steps", "3"], popen=popen)
+    out, err = capsys.readouterr()
+    assert rc == 0
+    assert out.strip() == '{"metric": "m", "value": 1.0, "n_gpus": 2}'
+    assert "noise from a rank" in err
+    cmd = seen["cmd"]
+    assert cmd[1:4] == ["-u", "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "2", "--steps", "3"] and cmd[-5].endswith("bench.py")
+
+
+def test_spawn_ranks_failure_modes(capsys):
+    assert bench.spawn_ranks(2, [], popen=lambda cmd, **kw: _FakeChild(["x\n"], 0)) == 1  # no result line
+    assert bench.spawn_ranks(2, [], popen=lambda cmd, **kw: _FakeChild([], 3)) == 3  # the child's code
+    capsys.readouterr()

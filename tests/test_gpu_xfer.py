@@ -87,3 +87,48 @@ def test_cache_clear_then_reuse(tqr, oracle):
     F = A.copy()
     T = tqr.geqrt_host(F, b)
     _check(F, T, F_ref, T_ref)
+
+
+def test_slow_host_staging_beyond_the_kernel_wait_limit(tqr, oracle):
+    """A host that stages the input slower than the engine's 5 s wait limit (one host
+    thread on a 32 GiB matrix): every tile column is staged 800 ms late (TQR_HOST_STAGE_DELAY_MS,
+    8 columns: 6.4 s), and the launch's waits on the host use its own, size-scaled limit."""
+    m, n, b = 512, 2048, 256
+    A = oracle.randzo(m, n, np.float64, seed=9)
+    F_ref, T_ref = oracle.factor(A, b)
+    os.environ["TQR_HOST_STAGE_DELAY_MS"] = "800"
+    try:
+        F = A.copy()
+        T = tqr.geqrt_host(F, b)
+    finally:
+        os.environ.pop("TQR_HOST_STAGE_DELAY_MS", None)
+    _check(F, T, F_ref, T_ref)
+
+
+def test_cache_clear_concurrent_with_calls(tqr, oracle):
+    """tqr_cache_clear while other threads run one-shot host-API calls on cached plans:
+    no call may use a freed plan or staging buffer, and every result stays exact."""
+    import threading
+    m = n = 512
+    b = 64
+    A = oracle.randzo(m, n, np.float64, seed=6)
+    F_ref, T_ref = oracle.factor(A, b)
+    errs = []
+
+    def worker():
+        try:
+            for _ in range(4):
+                F = A.copy()
+                T = tqr.geqrt_host(F, b)
+                _check(F, T, F_ref, T_ref)
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(e)
+
+    th = [threading.Thread(target=worker) for _ in range(2)]
+    for t in th:
+        t.start()
+    for _ in range(6):
+        tqr.cache_clear()
+    for t in th:
+        t.join()
+    assert not errs, errs
