@@ -921,7 +921,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
-    // next, err, wait limit (ms, flow.hpp timed_out), Rc, Tc, Ac, Rt, Rr, then Uc (upload chunks per tile column, host-pointer API)
+    // next, err, host-transfer progress (flow.hpp timed_out), Rc, Tc, Ac, Rt, Rr, then Uc (upload chunks per tile column, host-pointer API)
     pl->sync_ints = 3 + 3 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns +
                     (size_t)pl->kmax * pl->q * pl->ns * pl->ng + (size_t)pl->q;
     if (pl->nflow <= 0 || hipMalloc(&pl->d_flow, sizeof(Item) * pl->nflow) != hipSuccess ||
@@ -1220,13 +1220,6 @@ int tqr_plan_stats(const tqr_plan* pl, int* nu, double* msu, int* np, double* ms
 }
 
 static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_t cs, const XferArgs* xa = nullptr);
-// Wait limit of a host-pointer launch (flow.hpp timed_out): 5 s plus the matrix at 200 MB/s — the
-// host stages the input column by column while the launch runs, at whatever rate it gets (one
-// host thread, a busy host); the 5 s limit of device-resident launches would call that an error.
-static int host_wait_ms(const tqr_plan* pl) {
-  const double bytes = (double)pl->es * pl->m * pl->n;
-  return (int)std::min(2.0e9, 5000.0 + bytes / 200e3);
-}
 // Serialised enqueue of one execute (see tqr.h): the stream first waits for the plan's previous
 // execute; evDone marks this one. If enqueuing fails part-way, evDone is still recorded behind
 // whatever was enqueued (the wave engine's side streams are joined first), so the next execute
@@ -1274,8 +1267,6 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     }
     // multi-GPU: counters and flags are reset by tqr_dist_reset (all ranks, then a barrier)
     if (pl->world == 1) HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
-    // host-pointer API: every wait may depend on the host staging the input (see timed_out)
-    if (xa) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)(pl->d_sync + 2), host_wait_ms(pl), 1, cs));
     if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
     hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(FLOW_NT), pl->ldsF, cs, f);
     HIPCHK(hipGetLastError());

@@ -26,8 +26,8 @@
 //                 segment starts group g of its first element on it).
 // Deadlock freedom: every wait is on a task earlier in the list (host checks it), and tasks are
 // dequeued in list order, so the earliest unfinished dequeued task can always progress. Every
-// spin is bounded (FLOW_TIMEOUT, or the launch's own longer limit: timed_out); on timeout an error
-// word is set and all workgroups drain.
+// spin is bounded (FLOW_TIMEOUT without progress of the host transfers: timed_out); on timeout an
+// error word is set and all workgroups drain.
 #pragma once
 #include "tiles.hpp"
 
@@ -145,15 +145,23 @@ constexpr int FLOW_PT = TQR_POLL_T;
 #endif
 constexpr int FLOW_CHAIN_PT = TQR_CHAIN_PT;  // the fp64 chain's poll thread
 constexpr unsigned long long FLOW_TIMEOUT = 500000000ull;  // 5 s of s_memrealtime (100 MHz)
-// A wait gives up after FLOW_TIMEOUT, or after the launch's own limit if that is longer: the word
-// after the error word (err[1], milliseconds, written by the host before the launch; 0 = none).
-// The host-pointer API sets it from the matrix size — every wait there may depend on the host
-// staging the input column by column, which takes as long as the host needs (a 32 GiB matrix on
-// one host thread: several seconds). Read only once FLOW_TIMEOUT has passed (the cold path).
-__device__ __forceinline__ bool timed_out(unsigned long long el, int* err) {
-  if (el <= FLOW_TIMEOUT) return false;
-  const int ms = __hip_atomic_load((__attribute__((address_space(1))) int*)(err + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return el > (unsigned long long)(ms > 0 ? ms : 0) * 100000ull;
+// A wait gives up once FLOW_TIMEOUT has passed with no progress of the launch's host transfers:
+// the word after the error word (err[1]) counts the upload chunks done (xfer.hpp UP tasks; it
+// stays 0 on device-resident launches). With the host-pointer API every wait may depend on the
+// host staging the input column by column, as slowly as the host goes (a 32 GiB matrix on one host
+// thread takes several seconds); each expiry that finds the count moved restarts the wait.
+// last: the count seen at the previous expiry (0 before the first: device-resident launches keep
+// the 5 s limit). Cold path only.
+__device__ __forceinline__ bool timed_out(unsigned long long& t0, int& last, int* err) {
+  const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+  if (now - t0 <= FLOW_TIMEOUT) return false;
+  const int pr = __hip_atomic_load((__attribute__((address_space(1))) int*)(err + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (pr != last) {
+    last = pr;
+    t0 = now;
+    return false;
+  }
+  return true;
 }
 
 // Multi-GPU (tile-column cyclic partition, one process per GPU): peer buffers opened by IPC.
@@ -255,11 +263,12 @@ __device__ __forceinline__ T* uni(T* p) {
 // the poll wave's memory operations twice per group).
 __device__ __forceinline__ bool spin_ge_i(int* p, int target, int* err, bool sys = false) {
   if (ld_cnt(p, sys) >= target) return true;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  int last = 0;
   while (ld_cnt(p, sys) < target) {
     if (ld_relaxed(err)) return false;
     __builtin_amdgcn_s_sleep(8);
-    if (timed_out(__builtin_amdgcn_s_memrealtime() - t0, err)) {
+    if (timed_out(t0, last, err)) {
       __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
@@ -268,11 +277,12 @@ __device__ __forceinline__ bool spin_ge_i(int* p, int target, int* err, bool sys
 }
 __device__ __noinline__ bool spin_ge(int* p, int target, int* err, bool sys = false) {
   if (ld_cnt(p, sys) >= target) return true;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  int last = 0;
   while (ld_cnt(p, sys) < target) {
     if (ld_relaxed(err)) return false;
     __builtin_amdgcn_s_sleep(8);
-    if (timed_out(__builtin_amdgcn_s_memrealtime() - t0, err)) {
+    if (timed_out(t0, last, err)) {
       __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }

@@ -73,9 +73,9 @@ __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
 
-template <int B>
+template <int B, int IB_ = (B < 32 ? B : 32)>
 struct Geo {
-  static constexpr int IB = B < 32 ? B : 32;  // reflectors per group
+  static constexpr int IB = IB_;              // reflectors per group (default: 32, or B if smaller)
   static constexpr int NG = B / IB;           // groups per tile
   static constexpr int NKS = B / 4;           // 4-row k-steps over a tile
   static constexpr int NRI = IB / 4;          // 4-row blocks of a group
@@ -197,11 +197,12 @@ struct NoHook {
 // group's reflectors: T becomes block-upper-triangular at 8-reflector granularity, so W = -T^T Z
 // needs the k-blocks kb >= (wi & ~1) instead of kb >= wi (40 instead of 36 MFMAs per group).
 __device__ __forceinline__ constexpr int sigp(int r, int x) { return 8 * (r >> 1) + 2 * x + (r & 1); }
-template <int B, bool HEAD, typename Hook = NoHook, bool PF = true, bool TPACK = false, bool PAIRH = false>
+template <int B, bool HEAD, typename Hook = NoHook, bool PF = true, bool TPACK = false, bool PAIRH = false,
+          int IBX = Geo<B>::IB>
 __device__ __forceinline__ void apply_zw(const double* __restrict__ Vs, const double* __restrict__ Ts,
-                                         const double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI],
-                                         double (&W)[Geo<B>::NRI], int ks0, const Hook& hook = Hook()) {
-  using g = Geo<B>;
+                                         const double (&X)[Geo<B>::NKS], double (&H)[Geo<B, IBX>::NRI],
+                                         double (&W)[Geo<B, IBX>::NRI], int ks0, const Hook& hook = Hook()) {
+  using g = Geo<B, IBX>;
   constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP, TP = g::TP;
   const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
   double Z[NRI];
@@ -351,10 +352,10 @@ __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&
 // on its SIMD issues at 64 %, with 3-4 at 93-96 %, profiles/r02/ubench_mfma_f64_latency.txt —
 // the end of every group, when one wave of a pair has finished, runs on one wave). Operand
 // registers as apply_x: 4 k-steps x NRI/2 values, the next half read ahead.
-template <int B, typename Post = NoPost>
+template <int B, typename Post = NoPost, int IBX = Geo<B>::IB>
 __device__ __forceinline__ void apply_x4(const double* __restrict__ Vs, double (&X)[Geo<B>::NKS],
-                                         const double (&W)[Geo<B>::NRI], const Post& post = Post()) {
-  using g = Geo<B>;
+                                         const double (&W)[Geo<B, IBX>::NRI], const Post& post = Post()) {
+  using g = Geo<B, IBX>;
   constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP, NH = NRI / 2;
   static_assert(NKS % 4 == 0 && NH % 2 == 0, "apply_x4 blocks");
   const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
@@ -546,19 +547,19 @@ __device__ __forceinline__ unsigned head_off_pair(size_t ldm, int r0) {
   const int lane = threadIdx.x & 63, x = lane >> 4, c = lane & 15;
   return (unsigned)(((size_t)c * ldm + r0 + 2 * x) * sizeof(double));
 }
-template <int B, int AUX>
-__device__ __forceinline__ void load_head_pair(double (&H)[Geo<B>::NRI], __amdgpu_buffer_rsrc_t rs, unsigned base) {
+template <int B, int AUX, int IBX = Geo<B>::IB, int NRI_ = Geo<B, IBX>::NRI>
+__device__ __forceinline__ void load_head_pair(double (&H)[NRI_], __amdgpu_buffer_rsrc_t rs, unsigned base) {
 #pragma unroll
-  for (int h = 0; h < Geo<B>::NRI / 2; ++h) {
+  for (int h = 0; h < Geo<B, IBX>::NRI / 2; ++h) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 8 * h * 8, AUX);
     H[2 * h] = __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
     H[2 * h + 1] = __longlong_as_double((long long)(((unsigned long long)v[3] << 32) | v[2]));
   }
 }
-template <int B, int AUX>
-__device__ __forceinline__ void store_head_pair(const double (&H)[Geo<B>::NRI], __amdgpu_buffer_rsrc_t rs, unsigned base) {
+template <int B, int AUX, int IBX = Geo<B>::IB, int NRI_ = Geo<B, IBX>::NRI>
+__device__ __forceinline__ void store_head_pair(const double (&H)[NRI_], __amdgpu_buffer_rsrc_t rs, unsigned base) {
 #pragma unroll
-  for (int h = 0; h < Geo<B>::NRI / 2; ++h) {
+  for (int h = 0; h < Geo<B, IBX>::NRI / 2; ++h) {
     const unsigned long long a = (unsigned long long)__double_as_longlong(H[2 * h]);
     const unsigned long long b = (unsigned long long)__double_as_longlong(H[2 * h + 1]);
     __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
@@ -648,9 +649,9 @@ __device__ __forceinline__ void stage_t(double* Ts, const double* __restrict__ t
 
 // Packed T image: Tp[((kb * 4 + x) * 4 + y) * NRI + wi] = -T[4kb + x][4wi + y] (0 for wi < kb),
 // i.e. the A operands of W = -T^T Z for lane (x, y) and k-block kb, contiguous over wi.
-template <int B, int NTH>
+template <int B, int NTH, int IBX = Geo<B>::IB>
 __device__ __forceinline__ void pack_t(const double* Ts, double* Tp) {
-  using g = Geo<B>;
+  using g = Geo<B, IBX>;
   constexpr int NRI = g::NRI;
   for (int idx = threadIdx.x; idx < g::TPIMG; idx += NTH) {
     const int wi = idx % NRI, y = (idx / NRI) & 3, x = (idx / (4 * NRI)) & 3, kb = idx / (16 * NRI);
@@ -787,10 +788,10 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 //   3. the pivot's D_C and head_C are read from the owning lane (s_readlane, uniform);
 //   4. lane of column j forms f_j = tau (head_j + scale D_j) and publishes it wave-privately;
 //   5. rows update x_j -= f_j v (tails) / head_j -= f_j (GE head row, TS head in `hout`).
-template <int B, bool TS, int NW>
-__device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, double* Hs, double* tauv, double* red,
+template <int B, bool TS, int NW, int IBX = Geo<B>::IB>
+__device__ __forceinline__ void panel_step(double (&x)[IBX], double* Vs, double* Hs, double* tauv, double* red,
                                            double* wb, double* hrow, double* hout, int c0, int C, bool own, int rt) {
-  using g = Geo<B>;
+  using g = Geo<B, IBX>;
   constexpr int IB = g::IB, TP = g::TP, VP = g::VP;
   constexpr int SPAN = 64 / NW;  // lanes holding the same column after reduce-scatter
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -846,7 +847,7 @@ __device__ __forceinline__ void panel_step(double (&x)[Geo<B>::IB], double* Vs, 
   x[NW - 1] = 0.0;
   // GE: the next step's head row (updated just now as a tail) goes to the other hrow buffer
   // (every wave read this one's twin before passing this step's barrier)
-  if (!TS && C + 1 < Geo<B>::IB && rt == rc + 1) {
+  if (!TS && C + 1 < IBX && rt == rc + 1) {
     double2* hb = reinterpret_cast<double2*>(hrow + ((C + 1) & 1) * 32);
 #pragma unroll
     for (int h = 0; h < NW / 2; ++h) hb[h] = make_double2(x[2 * h], x[2 * h + 1]);
@@ -861,10 +862,10 @@ __device__ void panel_idle(const FwdJob* fj, int IB, bool TS);
 
 // PERM: LDS row q of Vs holds tile row vimg_row(q) (the chain engine's paired row order), else
 // tile row q. idle: optional work of waves 4-7 (8-wave engine), see FwdJob.
-template <int B, bool TS, bool PERM = false>
+template <int B, bool TS, bool PERM = false, int IBX = Geo<B>::IB>
 __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, double* scratch, int c0,
                                           const FwdJob* idle = nullptr) {
-  using g = Geo<B>;
+  using g = Geo<B, IBX>;
   constexpr int IB = g::IB, VP = g::VP, TP = g::TP;
   double* red = scratch;             // 2 x [4 waves][32] cross-wave partials (double-buffered)
   double* wb = red + 2 * 4 * 32;     // [4 waves][32] per-wave totals
@@ -897,10 +898,10 @@ __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, 
   // reduce the live window only: all IB columns while more than IB/2 are live, then the half
   constexpr int HALF = IB == 32 ? 16 : IB;
 #pragma clang loop unroll(disable)
-  for (int C = 0; C < HALF; ++C) panel_step<B, TS, IB>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
+  for (int C = 0; C < HALF; ++C) panel_step<B, TS, IB, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
   if constexpr (HALF < IB) {
 #pragma clang loop unroll(disable)
-    for (int C = HALF; C < IB; ++C) panel_step<B, TS, IB / 2>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
+    for (int C = HALF; C < IB; ++C) panel_step<B, TS, IB / 2, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
   }
   __syncthreads();
   if (TS) {
@@ -921,9 +922,9 @@ __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, 
 //     solved in parallel by back substitution, 8 lanes per column, DPP-reduced dot products.
 // Gs, Ts: IB x TP images. ks0: first non-zero 4-row block of V (GE), 0 for TS.
 // ---------------------------------------------------------------------------------------
-template <int B>
+template <int B, int IBX = Geo<B>::IB>
 __device__ __noinline__ void build_t(const double* Vs, const double* tauv, double* Gs, double* Ts, double* Gp, int ks0) {
-  using g = Geo<B>;
+  using g = Geo<B, IBX>;
   constexpr int IB = g::IB, VP = g::VP, TP = g::TP, NKS = g::NKS, NRI = g::NRI;
   constexpr int KPW = (NKS + 3) / 4;  // k-steps per wave
   constexpr int NCH = IB / 16;        // 16-column halves of the Gram

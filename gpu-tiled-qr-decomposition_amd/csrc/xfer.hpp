@@ -120,6 +120,8 @@ __device__ __noinline__ void flow_xfer(const FlowArgs& a, bool up, int j, int c,
   if (up) {
     xfer_columns<S, true>(a, B, j, r0, nr);
     wg_publish(&a.Uc[j], 1);  // sc1 stores drained, then one add
+    // host-transfer progress: waits that expire while it moves keep waiting (flow.hpp timed_out)
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(gptr(a.err + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     xfer_columns<S, false>(a, B, j, r0, nr);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
