@@ -269,8 +269,8 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
   const int P = uni(a.p), Q = uni(a.q), NS = uni(a.ns);
   int* const err = uni(a.err);
   int* const Tc = uni(a.Tc);
-  auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B, float>(P, i_, k, g_); };
-  auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B, float>(P, i_, k, g_); };
+  auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B, float, ShapeW8>(P, i_, k, g_); };
+  auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B, float, ShapeW8>(P, i_, k, g_); };
   int* const rc = uni(&a.Rc[(size_t)k * NG]);
   int* const acg = uni(&a.Ac[(((size_t)k * Q + j) * NS + s) * NG]);
   auto tc = [&](int i) { return &Tc[((size_t)i * Q + j) * NS + s]; };
@@ -325,8 +325,8 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
     FST(7);
     float* Xt = ts ? A + (size_t)j * B * ldm + (size_t)i * B : At;
     if (!dma_next) {
-      DmaJob<B, float> d{lds + buf * BUF, vimg(i, 0), timg(i, 0), sflag};
-      for (int m = 0; m < DmaJob<B, float>::STEPS; ++m) d.step(m);
+      DmaJob<B, float, ShapeW8> d{lds + buf * BUF, vimg(i, 0), timg(i, 0), sflag};
+      for (int m = 0; m < DmaJob<B, float, ShapeW8>::STEPS; ++m) d.step(m);
     }
     dma_next = false;
     const Strip32<B> xs(Xt, ldm, col);
@@ -410,7 +410,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
         const float* VRp = img;
         const float* TPi = img + 2 * Img<B, float>::V;
         const int gd = g + 1 < NG ? g + 1 : has_next ? 0 : g, id = g + 1 < NG ? i : has_next ? inext : i;
-        DmaJob<B, float> d{lds + (buf ^ 1) * BUF, vimg(id, gd), timg(id, gd), sflag};
+        DmaJob<B, float, ShapeW8> d{lds + (buf ^ 1) * BUF, vimg(id, gd), timg(id, gd), sflag};
         dma_next = g + 1 == NG && has_next;
 #if defined(TQR_DIAG_DMA_FIXED)  // what-if: every DMA reads one L2-hot image (results wrong)
         d.v = vimg(k, 0);
@@ -419,7 +419,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
 #ifdef TQR_DIAG_NODMA  // what-if: no staging at all (results wrong)
         const NoHook dh{};
 #else
-        const DmaJob<B, float>& dh = d;
+        const DmaJob<B, float, ShapeW8>& dh = d;
 #endif
         // (written before the sync; wave-uniform: a scalar branch around the hooked phase 2 — as a
         // per-lane value the two apply32 bodies became exec-masked twins, and at NG == 1 that
@@ -463,7 +463,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
             FST(13);
           }
         } else {
-          for (int m = 0; m < DmaJob<B, float>::STEPS; ++m) d.step(m);
+          for (int m = 0; m < DmaJob<B, float, ShapeW8>::STEPS; ++m) d.step(m);
         }
         if (g + 1 == NG) xin = pipe;
         buf ^= 1;

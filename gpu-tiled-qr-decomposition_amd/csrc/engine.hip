@@ -72,7 +72,9 @@ __device__ unsigned long long g_xtr[4096 * 8 * 8];  // its hand-over phase-2 mar
 #include "flow.hpp"
 namespace tqr {
 static_assert(FST_N <= 24, "g_fst holds 24 categories per workgroup");
-static_assert(Geo<256>::TPIMG == 1024 && Geo<16>::TPIMG == 256, "host tpimg_doubles mirrors Geo::TPIMG");
+static_assert(Geo<256>::TPIMG == 1024 && Geo<16>::TPIMG == 256 && Geo<256, 16>::TPIMG == 256 &&
+                  Geo<256, 16>::VIMG == 4608 && Geo<64, 16>::VIMG == 1152,
+              "host tpimg_doubles / vimg_doubles mirror Geo::TPIMG / VIMG");
 static_assert(Img<256, float>::V == 4096 && Img<256, float>::T == 384 && Img<16, float>::V == 128 && Img<16, float>::T == 128 &&
                   Img<64, float>::V == 1024 && Img<64, float>::T == 384,
               "host wk_bytes mirrors Img<B, float>");
@@ -312,23 +314,47 @@ static void get_kernels(kfn* p, kfn* u, kfn* t) {
   *t = k_build_t<B, S>;
 }
 typedef void (*ffn)(FlowArgs);
-template <int B, typename S>
-static ffn get_flow() { return k_flow<B, S>; }
-static size_t lds_flow(int b, int dtype) {
+// Engine shape of the persistent kernel (flow.hpp FlowShape): 4 = ShapeW4 (two 4-wave workgroups
+// per CU, 64-column strips, 16-reflector groups; the fp64 default), 8 = ShapeW8 (one 8-wave
+// workgroup per CU, 128-column strips, 32-reflector groups; fp32, and fp64 with TQR_FLOW_SHAPE=w8)
+struct ShapeInfo {
+  int nw, nt, sw, ib, wpc;
+};
+static ShapeInfo shape_info(int shape) {
+  return shape == 4 ? ShapeInfo{ShapeW4::NW, ShapeW4::NT, ShapeW4::SW, ShapeW4::IB, ShapeW4::WPC}
+                    : ShapeInfo{ShapeW8::NW, ShapeW8::NT, ShapeW8::SW, ShapeW8::IB, ShapeW8::WPC};
+}
+static int flow_shape(int dtype) {
+  if (dtype != TQR_F64) return 8;
+  const char* e = getenv("TQR_FLOW_SHAPE");
+  return e && strcmp(e, "w8") == 0 ? 8 : 4;
+}
+static int shape_ib(int shape, int b) { return std::min(b, shape_info(shape).ib); }
+static int shape_ns(int shape, int b) { const int sw = shape_info(shape).sw; return (b + sw - 1) / sw; }
+template <int B, typename S, class C>
+static ffn get_flow() { return k_flow<B, S, C>; }
+static size_t lds_flow(int b, int dtype, int shape) {
   int d = 0;
-#define TQR_L(BB) \
-  case BB: d = dtype == TQR_F64 ? flow_lds_doubles<BB, double>() : flow_lds_doubles<BB, float>(); break;
+#define TQR_L(BB)                                                                                  \
+  case BB:                                                                                         \
+    d = dtype != TQR_F64 ? flow_lds_doubles<BB, float, ShapeW8>()                                  \
+                         : shape == 4 ? flow_lds_doubles<BB, double, ShapeW4>() : flow_lds_doubles<BB, double, ShapeW8>(); \
+    break;
   switch (b) { TQR_L(16) TQR_L(32) TQR_L(64) TQR_L(128) TQR_L(256) }
 #undef TQR_L
   return (size_t)d * sizeof(double) + 1536;  // + task index, sync-point verdicts, Rc view, FST sums, wave sums
 }
-static ffn resolve_flow(int b, int dtype) {
+static ffn resolve_flow(int b, int dtype, int shape) {
   ffn f = nullptr;
-#define TQR_F(BB) \
-  case BB: f = dtype == TQR_F64 ? get_flow<BB, double>() : get_flow<BB, float>(); break;
+#define TQR_F(BB)                                                                                  \
+  case BB:                                                                                         \
+    f = dtype != TQR_F64 ? get_flow<BB, float, ShapeW8>()                                          \
+                         : shape == 4 ? get_flow<BB, double, ShapeW4>() : get_flow<BB, double, ShapeW8>(); \
+    break;
   switch (b) { TQR_F(16) TQR_F(32) TQR_F(64) TQR_F(128) TQR_F(256) }
 #undef TQR_F
-  if (f && hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_flow(b, dtype)) != hipSuccess)
+  if (f && hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_flow(b, dtype, shape)) !=
+               hipSuccess)
     return nullptr;
   return f;
 }
@@ -467,8 +493,10 @@ static int env_seglen() {
   return sl ? std::max(1, atoi(sl)) : 8;
 }
 
-static void build_flow_plan(int p, int q, int b, const FlowKnobs& kn, FlowPlan& fp, const XferPlan* xp = nullptr) {
-  const int kmax = std::min(p, q), ns = (b + FLOW_SW - 1) / FLOW_SW, ng = b / (b < 32 ? b : 32);
+// ns: chain strips per tile column, ng: reflector groups per tile (the engine shape's, shape_ns /
+// b / shape_ib)
+static void build_flow_plan(int p, int q, int ns, int ng, const FlowKnobs& kn, FlowPlan& fp, const XferPlan* xp = nullptr) {
+  const int kmax = std::min(p, q);
   // segment length per chain: shorter segments for the lookahead column pipeline consecutive
   // elements on different workgroups at reflector-group granularity
   auto seglen_of = [&](int k, int j) { return seglen_of_chain(k, j, kmax, kn.seglen, kn.seglen_la, kn.la_tail); };
@@ -652,17 +680,17 @@ static bool valid_b(int b) { return b == 16 || b == 32 || b == 64 || b == 128 ||
 // address at most 32 columns with 32-bit byte offsets (tiles.hpp load_strip_pair, flow.hpp):
 // 32 * ldm * es must stay below 2^31 (ldm <= 8,388,607 rows fp64, 16,777,215 fp32).
 static bool valid_ld(long ld, size_t es) { return ld > 0 && (size_t)32 * (size_t)ld * es <= 0x7fffffffull; }
-// workspace slot sizes (doubles) of Geo<b>::TIMG / VIMG
-static size_t timg_doubles(int b) {
-  const size_t ib = b < 32 ? b : 32;
-  return (ib * (ib + 1) + 127) / 128 * 128;
+// workspace slot sizes (doubles) of Geo<b, ib>::TIMG / VIMG / TPIMG (ib: reflectors per group)
+static size_t timg_doubles(int b, int ib = 32) {
+  ib = std::min(b, ib);
+  return ((size_t)ib * (ib + 1) + 127) / 128 * 128;
 }
-static size_t vimg_doubles(int b) {
-  const size_t ib = b < 32 ? b : 32;
+static size_t vimg_doubles(int b, int ib = 32) {
+  ib = std::min(b, ib);
   return ((size_t)b * (ib + 2) + 127) / 128 * 128;
 }
-static size_t tpimg_doubles(int b) {  // packed T image (Geo<b>::TPIMG)
-  const size_t nri = (b < 32 ? b : 32) / 4;
+static size_t tpimg_doubles(int b, int ib = 32) {  // packed T image (Geo<b, ib>::TPIMG)
+  const size_t nri = std::min(b, ib) / 4;
   return (16 * nri * nri + 127) / 128 * 128;
 }
 // fp32 chain image slots (doubles; tiles.hpp Geo32 / Img<B, float>)
@@ -671,10 +699,12 @@ static size_t timg32_doubles(int b) {
   const size_t nmi = (b < 32 ? b : 32) / 16, npr = nmi * (nmi + 1) / 2;
   return (npr * 256 / 2 + 127) / 128 * 128;
 }
-// flow engine workspace of one step with `rows` tile rows (flow.hpp flow_vw_off / flow_tw_off)
-static size_t wk_bytes(int b, int rows, int dtype) {
-  const size_t ng = b / (b < 32 ? b : 32);
-  const size_t slot = dtype == TQR_F64 ? vimg_doubles(b) + tpimg_doubles(b) : vimg32_doubles(b) + timg32_doubles(b);
+// flow engine workspace of one step with `rows` tile rows (flow.hpp flow_vw_off / flow_tw_off);
+// ib: the engine shape's group size (fp32: 32)
+static size_t wk_bytes(int b, int rows, int dtype, int ib) {
+  ib = std::min(b, ib);
+  const size_t ng = b / ib;
+  const size_t slot = dtype == TQR_F64 ? vimg_doubles(b, ib) + tpimg_doubles(b, ib) : vimg32_doubles(b) + timg32_doubles(b);
   return (size_t)rows * ng * slot * sizeof(double);
 }
 
@@ -703,6 +733,7 @@ struct tqr_plan {
   int* d_sync = nullptr;   // next, err, Rc, Tc, Ac, Rt, Rr
   size_t sync_ints = 0;
   int ns = 1, ng = 1, grid = 256, est_order = 0;
+  int shape = 8, nt = 512;  // flow engine shape (flow_shape) and its workgroup size
   ffn kflow = nullptr;
   size_t ldsF = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -912,12 +943,14 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     tqr_plan_destroy(pl); return TQR_EHIP;
   }
   // persistent dataflow engine: task list, progress counters, panel workspaces, kernel
-  pl->ns = (b + FLOW_SW - 1) / FLOW_SW;  // chain strips per tile
-  pl->ng = b / ib;
+  pl->shape = flow_shape(dtype);
+  pl->nt = shape_info(pl->shape).nt;
+  pl->ns = shape_ns(pl->shape, b);  // chain strips per tile
+  pl->ng = b / shape_ib(pl->shape, b);  // reflector groups per tile
   if (pl->engine == TQR_ENGINE_FLOW) {
     FlowPlan fp;
     pl->knobs = knobs_from_env(env_seglen());
-    build_flow_plan(pl->p, pl->q, b, pl->knobs, fp);
+    build_flow_plan(pl->p, pl->q, pl->ns, pl->ng, pl->knobs, fp);
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
@@ -938,7 +971,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     const bool wk_uc = world > 1 && !(getenv("TQR_DIST_WK_CACHED") && atoi(getenv("TQR_DIST_WK_CACHED")) == 1);
     for (int k = 0; k < pl->kmax; ++k) {
       double* w = nullptr;
-      const size_t wb = wk_bytes(b, pl->p - k, dtype);
+      const size_t wb = wk_bytes(b, pl->p - k, dtype, shape_ib(pl->shape, b));
       if ((wk_uc ? hipExtMallocWithFlags((void**)&w, wb, hipDeviceMallocUncached) : hipMalloc(&w, wb)) != hipSuccess) {
         tqr_plan_destroy(pl); return TQR_ENOMEM;
       }
@@ -959,14 +992,14 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
         tqr_plan_destroy(pl); return TQR_ENOMEM;
       }
     }
-    pl->kflow = resolve_flow(b, dtype);
-    pl->ldsF = lds_flow(b, dtype);
+    pl->kflow = resolve_flow(b, dtype, pl->shape);
+    pl->ldsF = lds_flow(b, dtype, pl->shape);
     int dev = 0;
     hipDeviceProp_t pr;
     if (!pl->kflow || hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&pr, dev) != hipSuccess) {
       tqr_plan_destroy(pl); return TQR_EHIP;
     }
-    pl->grid = pr.multiProcessorCount;
+    pl->grid = pr.multiProcessorCount * shape_info(pl->shape).wpc;  // (ShapeW4: two workgroups per CU)
     const char* gs = getenv("TQR_FLOW_GRID");
     if (gs) pl->grid = std::max(1, atoi(gs));
   }
@@ -1103,7 +1136,7 @@ long long tqr_plan_fwd_bytes(const tqr_plan* pl) {
   long long members = 0;  // panel members of the tile columns this rank owns
   for (int k = 0; k < pl->kmax; ++k)
     if (tile_owner(k, pl->world, pl->cyclic) == pl->rank) members += pl->p - k;
-  const long long slot = (long long)(wk_bytes(pl->b, 1, pl->dtype));  // one member's images, all groups
+  const long long slot = (long long)(wk_bytes(pl->b, 1, pl->dtype, shape_ib(pl->shape, pl->b)));  // one member's images, all groups
   return members * slot * (pl->world - 1);
 }
 
@@ -1112,10 +1145,15 @@ int tqr_dist_owner(const tqr_plan* pl, int tile_col) {
   return tile_owner(tile_col, pl->world, pl->cyclic);
 }
 
+// Host-only task-list helpers below describe the fp64 engine's list (flow_shape(TQR_F64)).
+static void host_flow_plan(int M, int N, int b, int seglen, FlowPlan& fp, const XferPlan* xp = nullptr) {
+  const int sh = flow_shape(TQR_F64);
+  build_flow_plan(M, N, shape_ns(sh, b), b / shape_ib(sh, b), knobs_from_env(seglen), fp, xp);
+}
 int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1 || world < 1 || rank < 0 || rank >= world) return TQR_EINVAL;
   FlowPlan fp;
-  build_flow_plan(M, N, b, knobs_from_env(seglen), fp);
+  host_flow_plan(M, N, b, seglen, fp);
   if (world > 1) partition_flow_plan(fp, rank, world);
   if (ntasks) *ntasks = (int)fp.items.size();
   if (nfwd) {  // panel members that forward their images (the panel tasks, when world > 1)
@@ -1127,13 +1165,13 @@ int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, in
   return TQR_OK;
 }
 
-int tqr_flow_strip_width(void) { return FLOW_SW; }
+int tqr_flow_strip_width(void) { return shape_info(flow_shape(TQR_F64)).sw; }
 
 int tqr_flow_order_check(int M, int N, int b, const int* items, int n) {
   if (M <= 0 || N <= 0 || !valid_b(b) || !items || n <= 0) return TQR_EINVAL;
   std::vector<Item> L(n);
   for (int x = 0; x < n; ++x) L[x] = Item{items[4 * x], items[4 * x + 1], items[4 * x + 2], items[4 * x + 3]};
-  return flow_list_topological(L, M, N, (b + FLOW_SW - 1) / FLOW_SW) ? 1 : 0;
+  return flow_list_topological(L, M, N, shape_ns(flow_shape(TQR_F64), b)) ? 1 : 0;
 }
 
 int tqr_plan_set_tasks(tqr_plan* pl, const int* items, int n) {
@@ -1156,7 +1194,7 @@ int tqr_plan_set_tasks(tqr_plan* pl, const int* items, int n) {
 
 int tqr_plan_debug_workspace(const tqr_plan* pl, int k, void* host, size_t bytes) {
   if (!pl || pl->engine != TQR_ENGINE_FLOW || k < 0 || k >= pl->kmax || !host) return TQR_EINVAL;
-  const size_t have = wk_bytes(pl->b, pl->p - k, pl->dtype);
+  const size_t have = wk_bytes(pl->b, pl->p - k, pl->dtype, shape_ib(pl->shape, pl->b));
   HIPCHK(hipMemcpy(host, pl->wk[k], std::min(bytes, have), hipMemcpyDeviceToHost));
   return (int)std::min<size_t>(have, 0x7fffffff);
 }
@@ -1164,7 +1202,7 @@ int tqr_plan_debug_workspace(const tqr_plan* pl, int k, void* host, size_t bytes
 int tqr_flow_plan_export(int M, int N, int b, int seglen, int* items, int cap) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1) return TQR_EINVAL;
   FlowPlan fp;
-  build_flow_plan(M, N, b, knobs_from_env(seglen), fp);
+  host_flow_plan(M, N, b, seglen, fp);
   const int n = (int)fp.items.size();
   if (items)
     for (int x = 0; x < n && x < cap; ++x) {
@@ -1177,7 +1215,7 @@ int tqr_flow_plan_export(int M, int N, int b, int seglen, int* items, int cap) {
 int tqr_flow_plan_check(int M, int N, int b, int seglen, int* ntasks, int* est_order) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1) return TQR_EINVAL;
   FlowPlan fp;
-  build_flow_plan(M, N, b, knobs_from_env(seglen), fp);
+  host_flow_plan(M, N, b, seglen, fp);
   if (ntasks) *ntasks = (int)fp.items.size();
   if (est_order) *est_order = fp.est_order;
   return TQR_OK;
@@ -1189,7 +1227,7 @@ int tqr_flow_xfer_plan_check(int M, int N, int b, int seglen, int nxc, double tc
   XferPlan xp;
   xp.nxc = nxc;
   xp.tcol = tcol;
-  build_flow_plan(M, N, b, knobs_from_env(seglen), fp, &xp);
+  host_flow_plan(M, N, b, seglen, fp, &xp);
   if (ntasks) *ntasks = (int)fp.items.size();
   if (est_order) *est_order = fp.est_order;
   return TQR_OK;
@@ -1268,7 +1306,7 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     // multi-GPU: counters and flags are reset by tqr_dist_reset (all ranks, then a barrier)
     if (pl->world == 1) HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
     if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
-    hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(FLOW_NT), pl->ldsF, cs, f);
+    hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(pl->nt), pl->ldsF, cs, f);
     HIPCHK(hipGetLastError());
     if (pl->profile) {
       HIPCHK(hipEventRecord(pl->ev1, cs));
@@ -1563,14 +1601,14 @@ static int plan_xfer_list(tqr_plan* pl) {
   xrows = std::min(pl->m, std::max(xrows, ((pl->m + 254) / 255 + 3) & ~3));
   XferPlan xp;
   xp.nxc = (pl->m + xrows - 1) / xrows;
-  // estimator unit = one chain element (4 b^2 FLOW_SW flop at ~1/256 of the chip); a tile column
-  // over PCIe at TQR_XFER_GBS (default 45 GB/s)
+  // estimator unit = one chain element (4 b^2 SW flop at ~1/256 of the chip, SW the shape's strip
+  // width); a tile column over PCIe at TQR_XFER_GBS (default 45 GB/s)
   const char* eg = getenv("TQR_XFER_GBS");
   const double gbs = eg ? std::max(1.0, atof(eg)) : 45.0;
-  const double elem_s = 4.0 * pl->b * pl->b * FLOW_SW / (pl->dtype == TQR_F64 ? 0.175e12 : 0.38e12);
+  const double elem_s = 4.0 * pl->b * pl->b * shape_info(pl->shape).sw / (pl->dtype == TQR_F64 ? 0.175e12 : 0.38e12);
   xp.tcol = ((double)pl->m * pl->b * pl->es / (gbs * 1e9)) / elem_s;
   FlowPlan fp;
-  build_flow_plan(pl->p, pl->q, pl->b, pl->knobs, fp, &xp);  // the plan's own knobs (not the environment now)
+  build_flow_plan(pl->p, pl->q, pl->ns, pl->ng, pl->knobs, fp, &xp);  // the plan's own knobs (not the environment now)
   Item* d = nullptr;
   if (hipMalloc(&d, sizeof(Item) * fp.items.size()) != hipSuccess) return TQR_ENOMEM;
   if (hipMemcpy(d, fp.items.data(), sizeof(Item) * fp.items.size(), hipMemcpyHostToDevice) != hipSuccess) {

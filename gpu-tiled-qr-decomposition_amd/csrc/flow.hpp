@@ -120,6 +120,23 @@ constexpr int FLOW_NT = 512;
 constexpr int FLOW_NW = FLOW_NT / 64;      // waves
 constexpr int FLOW_SW = 16 * FLOW_NW;      // strip width (columns) of a chain task
 constexpr bool FLOW_PF = true;
+
+// Engine shapes. ShapeW8 is the form above (one 8-wave workgroup per CU, 128-column chain strips,
+// 32-reflector groups): the fp32 engine, and fp64 under TQR_FLOW_SHAPE=w8. ShapeW4 (round 4, the
+// fp64 default): TWO independent 4-wave workgroups per CU, 64-column chain strips, 16-reflector
+// groups — half the LDS images (76 KiB per workgroup, so two fit in the CU's 160 KiB), and the two
+// workgroups run different tasks: one's strip hand-over (its stores' acknowledgement on the shared
+// vmcnt), barrier skew and dependent-MFMA tails run beside the other's MFMA stream instead of
+// idling the CU's matrix pipes (tools/ubench/chain2_bench.hip).
+template <int NW_, int IB_, int WPC_>
+struct FlowShape {
+  static constexpr int NW = NW_, NT = 64 * NW_, SW = 16 * NW_, IB = IB_, WPC = WPC_;
+};
+using ShapeW8 = FlowShape<8, 32, 1>;
+using ShapeW4 = FlowShape<4, 16, 2>;
+// the tile geometry a shape runs at (groups of min(B, IB) reflectors)
+template <int B, class C>
+using FGeo = Geo<B, (B < C::IB ? B : C::IB)>;
 // cache policy of the chain's in-segment head-row traffic (buffer aux bits; 16 = sc1, 2 = nt)
 #ifndef TQR_HEAD_ST_AUX
 #define TQR_HEAD_ST_AUX 0
@@ -143,7 +160,10 @@ constexpr int FLOW_PT = TQR_POLL_T;
 #ifndef TQR_CHAIN_PT
 #define TQR_CHAIN_PT 448
 #endif
-constexpr int FLOW_CHAIN_PT = TQR_CHAIN_PT;  // the fp64 chain's poll thread
+constexpr int FLOW_CHAIN_PT = TQR_CHAIN_PT;  // the fp64 chain's poll thread (ShapeW8)
+// ShapeW4: the last wave's first lane (as wave 7 of the 8-wave form)
+template <class C>
+__device__ constexpr int chain_pt() { return C::NW == 8 ? FLOW_CHAIN_PT : C::NT - 64; }
 constexpr unsigned long long FLOW_TIMEOUT = 500000000ull;  // 5 s of s_memrealtime (100 MHz)
 // A wait gives up once FLOW_TIMEOUT has passed with no progress of the launch's host transfers:
 // the word after the error word (err[1]) counts the upload chunks done (xfer.hpp UP tasks; it
@@ -326,22 +346,30 @@ __device__ __forceinline__ void wg_publish(int* p, int delta, bool sys = false) 
   }
 }
 
-template <int B, typename S>
+// workspace slot sizes (doubles) of one reflector group's images in a shape: fp64 storage = the
+// fp64 chain's V image + packed T at the shape's group size; fp32 storage = the fp32 chain's
+// images (tiles.hpp Img, 32-reflector groups)
+template <int B, typename S, class C>
+struct FImg {
+  static constexpr int V = sizeof(S) == 8 ? FGeo<B, C>::VIMG : Img<B, S>::V;
+  static constexpr int T = sizeof(S) == 8 ? FGeo<B, C>::TPIMG : Img<B, S>::T;
+};
+template <int B, typename S, class C>
 __device__ __forceinline__ size_t flow_vw_off(int p, int i, int k, int g) {
-  return ((size_t)(i - k) * Geo<B>::NG + g) * Img<B, S>::V;
+  return ((size_t)(i - k) * FGeo<B, C>::NG + g) * FImg<B, S, C>::V;
 }
-template <int B, typename S>
+template <int B, typename S, class C>
 __device__ __forceinline__ size_t flow_tw_off(int p, int i, int k, int g) {
-  constexpr int NG = Geo<B>::NG;
-  return (size_t)(p - k) * NG * Img<B, S>::V + ((size_t)(i - k) * NG + g) * Img<B, S>::T;
+  constexpr int NG = FGeo<B, C>::NG;
+  return (size_t)(p - k) * NG * FImg<B, S, C>::V + ((size_t)(i - k) * NG + g) * FImg<B, S, C>::T;
 }
-template <int B, typename S>
+template <int B, typename S, class C>
 __device__ __forceinline__ double* flow_tw(const FlowArgs& a, int i, int k, int g) {
-  return a.Wk[k] + flow_tw_off<B, S>(a.p, i, k, g);
+  return a.Wk[k] + flow_tw_off<B, S, C>(a.p, i, k, g);
 }
-template <int B, typename S>
+template <int B, typename S, class C>
 __device__ __forceinline__ double* flow_vw(const FlowArgs& a, int i, int k, int g) {
-  return a.Wk[k] + flow_vw_off<B, S>(a.p, i, k, g);
+  return a.Wk[k] + flow_vw_off<B, S, C>(a.p, i, k, g);
 }
 
 // ---- LDS-DMA staging of one reflector group ------------------------------------------------
@@ -354,11 +382,12 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 // DMA job of one group for apply_zw's hook: step m issues this wave's m-th LDS-DMA instruction
 // (V image instructions first, then T), so the issue cost hides under the MFMA stream.
-template <int B, typename S = double>
+template <int B, typename S = double, class C = ShapeW8>
 struct DmaJob {
-  static constexpr int VIMG = Img<B, S>::V;
-  static constexpr int NIV = Img<B, S>::V / 128, NIT = Img<B, S>::T / 128;
-  static constexpr int PV = (NIV + FLOW_NW - 1) / FLOW_NW, PT = (NIT + FLOW_NW - 1) / FLOW_NW;
+  static constexpr int NW = C::NW;
+  static constexpr int VIMG = FImg<B, S, C>::V;
+  static constexpr int NIV = FImg<B, S, C>::V / 128, NIT = FImg<B, S, C>::T / 128;
+  static constexpr int PV = (NIV + NW - 1) / NW, PT = (NIT + NW - 1) / NW;
   static constexpr int STEPS = PV + PT;
   double* dst;
   const double* v;
@@ -373,10 +402,10 @@ struct DmaJob {
     // wave id made provably uniform: addresses = scalar base + one per-lane offset register
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (m < PV) {
-      const int u = min(w + FLOW_NW * m, NIV - 1);
+      const int u = min(w + NW * m, NIV - 1);
       dma16(v + u * 128 + 2 * lane, dst + u * 128);
     } else if (m < STEPS) {
-      const int u = min(w + FLOW_NW * (m - PV), NIT - 1);
+      const int u = min(w + NW * (m - PV), NIT - 1);
       dma16(t + u * 128 + 2 * lane, dst + VIMG + u * 128);
     }
   }
@@ -401,7 +430,7 @@ struct DmaJob {
 // every sync point there drains fully anyway).
 template <bool DRAIN, bool FLAT = false, int PT = FLOW_PT>
 __device__ __forceinline__ bool sync_point(bool ok0, int* sflag, int& par) {
-  int* slot = sflag + 40 + par;  // LDS tail (ints from the task word): [task][flag][..][verdicts 41,42][..][Rc view 49..][..][FST sums 64..]
+  int* slot = sflag + 40 + par;  // LDS tail (ints from the task word): [task][flag][..][verdicts 41,42][..][Rc view 49.. (fp32) / 261.. (fp64)][..][FST sums 64..]
   par ^= 1;
   if (threadIdx.x == PT) *lds_int(slot) = ok0 ? 1 : 0;
   WST_T0();
@@ -567,7 +596,7 @@ __device__ __noinline__ void write_images32(const double* Vs, const double* Ts, 
 // system scope and sets the peers' member flags Rf[k][i][g]. (Round 2 had a separate forward
 // task per member, dequeued right behind it: it held a workgroup while waiting for the member's
 // groups — 5.4 % of workgroup time in the 2-rank rehearsal, 682 vs 667 ms for this form.)
-template <int B, typename S>
+template <int B, typename S, class C>
 __device__ __forceinline__ void fwd_images(const FlowArgs& a, int k, size_t vo, size_t to) {
   const __amdgpu_buffer_rsrc_t vsrc = uniform_rsrc(a.Wk[k] + vo), tsrc = uniform_rsrc(a.Wk[k] + to);
   for (int r = 0; r < a.world; ++r) {
@@ -575,9 +604,9 @@ __device__ __forceinline__ void fwd_images(const FlowArgs& a, int k, size_t vo, 
     double* pw = a.peers[r].Wk[k];
     const __amdgpu_buffer_rsrc_t vdst = uniform_rsrc(pw + vo), tdst = uniform_rsrc(pw + to);
 #pragma unroll 4
-    for (int c = threadIdx.x; c < Img<B, S>::V / 2; c += blockDim.x)
+    for (int c = threadIdx.x; c < FImg<B, S, C>::V / 2; c += blockDim.x)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(vsrc, 16 * c, 0, 16), vdst, 16 * c, 0, 17);
-    for (int c = threadIdx.x; c < Img<B, S>::T / 2; c += blockDim.x)
+    for (int c = threadIdx.x; c < FImg<B, S, C>::T / 2; c += blockDim.x)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_amdgcn_raw_buffer_load_b128(tsrc, 16 * c, 0, 16), tdst, 16 * c, 0, 17);
   }
 }
@@ -652,9 +681,10 @@ __device__ __noinline__ void panel_idle(const FwdJob* fjp, int IB, bool TS) {
 }
 
 // ---- panel tasks ---------------------------------------------------------------------------
-template <int B, typename S>
+template <int B, typename S, class C>
 __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* lds, int* sflag) {
-  using G = Geo<B>;
+  using G = FGeo<B, C>;
+  constexpr int NT = C::NT;
   constexpr int IB = G::IB, VP = G::VP, TP = G::TP, NG = G::NG;
   double* Vs = lds;
   double* Hs = Vs + G::VSZ;
@@ -698,7 +728,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt + (size_t)c0 * ldm);  // offsets span IB columns
       const int rlo = qrs ? c0 : 0;
 #pragma unroll 4
-      for (int idx = t; idx < B * IB / 2; idx += FLOW_NT) {
+      for (int idx = t; idx < B * IB / 2; idx += NT) {
         const int r = 2 * (idx % (B / 2)), c = idx / (B / 2);
         double v0 = 0.0, v1 = 0.0;
         if (r >= rlo) ld_pair<S>(rs, (unsigned)(((size_t)c * ldm + r) * sizeof(S)), v0, v1);
@@ -707,7 +737,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       }
     }
     if (!qrs) {
-      for (int idx = t; idx < IB * IB; idx += FLOW_NT) {
+      for (int idx = t; idx < IB * IB; idx += NT) {
         const int r = idx % IB, c = idx / IB;
         if (r <= c) Hs[r * TP + c] = ldc(Rt + (size_t)(c0 + c) * ldm + c0 + r);
       }
@@ -717,19 +747,20 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     // Vs holds the panel rows in the chains' paired order (LDS row q = tile row vimg_row(q)): the
     // V image is then a verbatim copy and the trailing update moves 16-B row pairs
     // multi-GPU: waves 4-7 forward group g-1's images meanwhile (FwdJob)
-    const FwdJob fj{&a, k, flow_vw_off<B, S>(a.p, me, k, g - 1), flow_tw_off<B, S>(a.p, me, k, g - 1),
-                    ((size_t)k * a.p + me) * NG + g - 1, Img<B, S>::V / 2, Img<B, S>::T / 2, sflag + 36};
-    const FwdJob* fjp = a.dist && g > 0 ? &fj : nullptr;
+    // (ShapeW4 has no idle waves: every group is forwarded inline, below)
+    const FwdJob fj{&a, k, flow_vw_off<B, S, C>(a.p, me, k, g - 1), flow_tw_off<B, S, C>(a.p, me, k, g - 1),
+                    ((size_t)k * a.p + me) * NG + g - 1, FImg<B, S, C>::V / 2, FImg<B, S, C>::T / 2, sflag + 36};
+    const FwdJob* fjp = a.dist && g > 0 && NT > 256 ? &fj : nullptr;
 #ifndef TQR_DIAG_NOPFACT  // what-if: no panel factorisation (results wrong)
-    if (qrs) panel_factor<B, false, true>(Vs, Hs, tauv, scratch, c0, fjp);
-    else panel_factor<B, true, true>(Vs, Hs, tauv, scratch, c0, fjp);
+    if (qrs) panel_factor<B, false, true, IB>(Vs, Hs, tauv, scratch, c0, fjp);
+    else panel_factor<B, true, true, IB>(Vs, Hs, tauv, scratch, c0, fjp);
 #endif
     FST(5);
     {  // write-back of the factored block (R / V), row pairs as 16-B write-through stores
       const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt + (size_t)c0 * ldm);
       const int rlo = qrs ? c0 : 0;
 #pragma unroll 4
-      for (int idx = t; idx < B * IB / 2; idx += FLOW_NT) {
+      for (int idx = t; idx < B * IB / 2; idx += NT) {
         const int r = 2 * (idx % (B / 2)), c = idx / (B / 2);
         if (r >= rlo)
           st_pair<S>(rs, (unsigned)(((size_t)c * ldm + r) * sizeof(S)), Vs[vimg_inv(r) * VP + G::pc(c)],
@@ -737,7 +768,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       }
     }
     if (!qrs) {
-      for (int idx = t; idx < IB * IB; idx += FLOW_NT) {
+      for (int idx = t; idx < IB * IB; idx += NT) {
         const int r = idx % IB, c = idx / IB;
         if (r <= c) st(Rt + (size_t)(c0 + c) * ldm + c0 + r, Hs[r * TP + c]);
       }
@@ -745,7 +776,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     if (t < IB) st(tau + (size_t)k * a.m + (size_t)(qrs ? k : l) * B + c0 + t, tauv[t]);
     wg_publish(&a.Rr[(size_t)k * NG + g], 1);  // includes the drain and the barrier
     if (qrs) {
-      for (int idx = t; idx < B * IB; idx += FLOW_NT) {
+      for (int idx = t; idx < B * IB; idx += NT) {
         const int r = idx % B, c = idx / B, d = c0 + c;
         if (r <= d) Vs[vimg_inv(r) * VP + G::pc(c)] = r == d ? 1.0 : 0.0;
       }
@@ -753,16 +784,16 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     }
     FST(10);
 #ifndef TQR_DIAG_NOBT  // what-if: no T formation (results wrong)
-    build_t<B>(Vs, tauv, Gs, Ts, Gp, 0);  // (permuted rows: the GE zero rows are not a prefix)
+    build_t<B, IB>(Vs, tauv, Gs, Ts, Gp, 0);  // (permuted rows: the GE zero rows are not a prefix)
 #endif
     // packed T (the Gram buffer is free now): the trailing update's and the chains' T operand
     double* Tp = Gs;
-    pack_t<B, FLOW_NT>(Ts, Tp);
+    pack_t<B, NT, IB>(Ts, Tp);
     __syncthreads();
     FST(11);
     {  // V image (explicit) and packed T image of this group for the chains (LDS-DMA sources)
-      double* tg = flow_tw<B, S>(a, qrs ? k : l, k, g);
-      double* vg = flow_vw<B, S>(a, qrs ? k : l, k, g);
+      double* tg = flow_tw<B, S, C>(a, qrs ? k : l, k, g);
+      double* vg = flow_vw<B, S, C>(a, qrs ? k : l, k, g);
       const __amdgpu_buffer_rsrc_t rv = uniform_rsrc(vg), rt = uniform_rsrc(tg);
       if constexpr (sizeof(S) == 8) {
         // the chain's images in the paired reflector order (tiles.hpp sigp): V image position
@@ -776,8 +807,8 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
           const int row = e / VP, pos = e % VP;
           return pos < IB ? Vs[row * VP + G::pc(sigp(pos % NRI, pos / NRI))] : 0.0;
         };
-        for (int idx = t; idx < G::TPIMG / 2; idx += FLOW_NT) st_pair<double>(rt, 16 * idx, tpk(2 * idx), tpk(2 * idx + 1));
-        for (int idx = t; idx < G::VSZ / 2; idx += FLOW_NT) st_pair<double>(rv, 16 * idx, vim(2 * idx), vim(2 * idx + 1));
+        for (int idx = t; idx < G::TPIMG / 2; idx += NT) st_pair<double>(rt, 16 * idx, tpk(2 * idx), tpk(2 * idx + 1));
+        for (int idx = t; idx < G::VSZ / 2; idx += NT) st_pair<double>(rv, 16 * idx, vim(2 * idx), vim(2 * idx + 1));
       } else {
         write_images32<B>(Vs, Ts, rv, rt);  // the fp32 chain's operand images (chain32.hpp)
       }
@@ -785,9 +816,11 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
     wg_publish(&a.Rc[(size_t)k * NG + g], 1);
     FST(10);
-    // multi-GPU, last group: the images to every peer now (drained by the Rt publish below, flags
-    // after it); earlier groups go during the next group's factorisation (FwdJob)
-    if (a.dist && g + 1 == NG) fwd_images<B, S>(a, k, flow_vw_off<B, S>(a.p, me, k, g), flow_tw_off<B, S>(a.p, me, k, g));
+    // multi-GPU, last group (every group in ShapeW4): the images to every peer now (drained by the
+    // Rt publish below, flags after it); earlier groups go during the next group's factorisation
+    // (FwdJob, waves 4-7 of ShapeW8)
+    const bool fwd_inline = a.dist && (g + 1 == NG || NT <= 256);
+    if (fwd_inline) fwd_images<B, S, C>(a, k, flow_vw_off<B, S, C>(a.p, me, k, g), flow_tw_off<B, S, C>(a.p, me, k, g));
     FST(23);
     if (!qrs) {  // R_kk head rows right of the group as left by the previous member's trailing
       const bool ok = t == FLOW_PT ? spin_ge(&a.Rt[(size_t)k * NG + g], pos, a.err) : true;
@@ -803,29 +836,29 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     // see flow_chain's UNMQR element.
     const int h0 = qrs ? c0 / 8 : 0;
 #ifdef TQR_DIAG_NOPTRAIL  // what-if: no in-tile trailing update (results wrong)
-    for (int s = nstr; s < nstr; s += FLOW_NT / 64) {
+    for (int s = nstr; s < nstr; s += C::NW) {
 #else
-    for (int s = w; s < nstr; s += FLOW_NT / 64) {
+    for (int s = w; s < nstr; s += C::NW) {
 #endif
       asm volatile("" ::: "memory");
       const int col = c0 + IB + 16 * s;
       const __amdgpu_buffer_rsrc_t rsH = head_rsrc(Rt + (size_t)col * ldm, !qrs);
       const unsigned so = head_off<B, S>(ldm, c0);  // head row c0 + x, column col + lane's
       load_strip_pair<B, S>(X, Bt, ldm, col, h0);
-      load_head_buf<B, S, 16>(H, rsH, so);
+      load_head_buf<B, S, 16, IB>(H, rsH, so);
 #ifdef TQR_FLOW_STAMPS
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
       FST(16);
-      apply_group<B, true, FLOW_PF, true>(Vs, Tp, X, H, 0);
+      apply_group<B, true, FLOW_PF, true, IB>(Vs, Tp, X, H, 0);
       FST(12);
       store_strip_pair<B, S>(X, Bt, ldm, col, h0);
-      store_head_buf<B, S, 16>(H, rsH, so);
+      store_head_buf<B, S, 16, IB>(H, rsH, so);
       FST(17);
     }
     wg_publish(&a.Rt[(size_t)k * NG + g], 1);
     FST(12);
-    if (a.dist && g + 1 == NG && t == 0) {  // every wave's peer stores drained (the Rt publish): release, flags
+    if (fwd_inline && t == 0) {  // every wave's peer stores drained (the Rt publish): release, flags
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const size_t fo = ((size_t)k * a.p + me) * NG + g;
@@ -842,7 +875,9 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
 // barrier while its partner ran alone, every dependency and LDS bubble of a single wave exposed
 // (stamps: waves 1-3 waited 44 ms per workgroup at the barriers, waves 5-7 11 ms). Phase 1
 // favours the upper waves, phase 2 the lower ones, so the pair ends its group together.
+template <class C>
 __device__ __forceinline__ void phase_prio(bool phase2) {
+  if constexpr (C::NW < 8) return;  // ShapeW4: the SIMD's other wave belongs to another workgroup
 #ifndef TQR_NO_PRIO
   const bool upper = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4;
   if (upper != phase2) __builtin_amdgcn_s_setprio(1);
@@ -909,25 +944,27 @@ struct XPipe {
 //   its MFMA stream into the other LDS buffer.
 // The tile-strip counter Tc of an element is published after the next element's first drain
 // (its stores are complete by then), so no wave waits for its own stores to land.
-template <int B, typename S>
+template <int B, typename S, class C>
 __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int i1_, int j_, int k_, int seg_,
                                         double* lds, int* sflag) {
   const int s = uni(s_), i0 = uni(i0_), i1 = uni(i1_), j = uni(j_), k = uni(k_), seg = uni(seg_);
-  using G = Geo<B>;
+  using G = FGeo<B, C>;
   constexpr int IB = G::IB, NG = G::NG, BUF = G::VIMG + G::TPIMG;
+  constexpr int SW = C::SW;
+  using Dma = DmaJob<B, S, C>;
   // (uniform: per-lane copies were spilled, and their reload at every element start waited for
   // vmcnt(0) — behind the previous element's whole strip hand-over)
   S* A = uni((S*)a.A);
   const size_t ldm = uni64(a.ldm);
   const int t = threadIdx.x, w = t >> 6;
-  constexpr int PT = FLOW_CHAIN_PT;
+  constexpr int PT = chain_pt<C>();
   constexpr int HPACK = 2;  // head rows per lane and access (16-B paired head rows, tiles.hpp sigp)
-  const int col = s * FLOW_SW + 16 * w;  // this wave's 16 columns inside the tile
+  const int col = s * SW + 16 * w;  // this wave's 16 columns inside the tile
   // byte-free element offset of the wave's first column, made uniform: as a per-lane product the
   // strip / head base pointers derived from it were VGPR pairs, spilled, and reloaded at every
   // element start behind an s_waitcnt vmcnt(0) (a full drain of the previous hand-over)
   const size_t colo = uni64((size_t)col * ldm);
-  const bool active = B % FLOW_SW == 0 || col < B;  // (compile-time true unless B < FLOW_SW)
+  const bool active = B % SW == 0 || col < B;  // (compile-time true unless B < SW)
   S* At = A + (size_t)j * B * ldm + (size_t)k * B;  // tile (k,j): the chain's head rows
   // everything the group loop needs from FlowArgs, read once per task: the asm memory clobbers
   // of the sync points would otherwise force a reload per group — for Wk[k] a global load whose
@@ -936,8 +973,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   const int P = uni(a.p), Q = uni(a.q), NS = uni(a.ns);
   int* const err = uni(a.err);
   int* const Tc = uni(a.Tc);
-  auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B, S>(P, i_, k, g_); };
-  auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B, S>(P, i_, k, g_); };
+  auto vimg = [&](int i_, int g_) { return wk + flow_vw_off<B, S, C>(P, i_, k, g_); };
+  auto timg = [&](int i_, int g_) { return wk + flow_tw_off<B, S, C>(P, i_, k, g_); };
   int* const rc = uni(&a.Rc[(size_t)k * NG]);
   int* const acg = uni(&a.Ac[(((size_t)k * Q + j) * NS + s) * NG]);  // per head-row group
   auto tc = [&](int i) { return &Tc[((size_t)i * Q + j) * NS + s]; };
@@ -950,7 +987,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   // sync point tests (sflag[57]), the Tc of the next element's tile, loaded two groups ahead
   // (sflag[58]; -1: none), the member flag of a remote panel (sflag[59])
   PanelView<NG, PT> pv;
-  pv.init(sflag + 48, sflag + 57);
+  // (the Rc view holds NG words: up to 16 at 16-reflector groups, past the stamps' LDS words)
+  static_assert(NG <= 16, "LDS tail: Rc view of at most 16 groups");
+  pv.init(sflag + 260, sflag + 57);
   int* const tcs = sflag + 58;
   int* const fls = sflag + 59;
   int* const acs = sflag + 60;  // Ac[g+1] of a later segment's first element, loaded a group ahead
@@ -994,8 +1033,8 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     FST(7);
     S* Xt = ts ? A + (size_t)j * B * ldm + (size_t)i * B : At;
     if (!dma_next) {  // (first: the strip and head loads must be the youngest, see sync_point_first)
-      DmaJob<B> d{lds + buf * BUF, vimg(i, 0), timg(i, 0), sflag};
-      for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
+      Dma d{lds + buf * BUF, vimg(i, 0), timg(i, 0), sflag};
+      for (int m = 0; m < Dma::STEPS; ++m) d.step(m);
     }
     dma_next = false;
     // head rows: written by another workgroup before this segment or by this one (sc1 loads
@@ -1008,7 +1047,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     // loop, and that copy waits for them — issued after the strip it waited for the whole strip.
     const __amdgpu_buffer_rsrc_t hrs = head_rsrc(At + colo, ts);  // UNMQR: empty resource, head = 0
     const unsigned hoff = head_off_pair<B>(ldm, 0);
-    if (FLOW_PF && active) load_head_pair<B, TQR_HEAD_LD0_AUX>(H, hrs, hoff);
+    if (FLOW_PF && active) load_head_pair<B, TQR_HEAD_LD0_AUX, IB>(H, hrs, hoff);
 #ifndef TQR_DIAG_NOSTRIP
     if (active && !xin) load_strip_pair<B, S>(X, Xt + colo, ldm, 0);
 #endif
@@ -1100,27 +1139,27 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         if (i == ifirst && seg > 0 && g + 2 < NG) lds_prefetch<PT>(&acg[g + 2], acs, false);
       }
       FST(7);
-      if (!FLOW_PF && active) load_head_pair<B, 16>(H, hrs, hoff + g * IB * sizeof(S));
+      if (!FLOW_PF && active) load_head_pair<B, 16, IB>(H, hrs, hoff + g * IB * sizeof(S));
       const double* Vs = lds + buf * BUF;
       const double* Ts = Vs + G::VIMG;
       // the other buffer is free (every wave passed this sync point): next DMA rides phase 1
       // (nothing next: re-read this group's own images into the idle buffer, keeping the
       // DMA stream branch-free)
       const int gd = g + 1 < NG ? g + 1 : has_next ? 0 : g, id = g + 1 < NG ? i : has_next ? inext : i;
-      DmaJob<B> d{lds + (buf ^ 1) * BUF, vimg(id, gd), timg(id, gd), sflag};
+      Dma d{lds + (buf ^ 1) * BUF, vimg(id, gd), timg(id, gd), sflag};
       dma_next = g + 1 == NG && has_next;
 #if defined(TQR_DIAG_DMA_FIXED)  // what-if: every DMA reads one L2-hot image
       d.v = vimg(k, 0);
       d.t = timg(k, 0);
 #endif
 #ifdef TQR_DIAG_NODMA  // what-if: no staging at all
-      if (active) apply_zw<B, true, NoHook, FLOW_PF, true, HPACK == 2>(Vs, Ts, X, H, W, 0);
+      if (active) apply_zw<B, true, NoHook, FLOW_PF, true, HPACK == 2, IB>(Vs, Ts, X, H, W, 0);
 #else
-      phase_prio(false);
+      phase_prio<C>(false);
       WMARK(3);
-      if (active) apply_zw<B, true, DmaJob<B>, FLOW_PF, true, HPACK == 2>(Vs, Ts, X, H, W, 0, d);
+      if (active) apply_zw<B, true, Dma, FLOW_PF, true, HPACK == 2, IB>(Vs, Ts, X, H, W, 0, d);
       else
-        for (int m = 0; m < DmaJob<B>::STEPS; ++m) d.step(m);
+        for (int m = 0; m < Dma::STEPS; ++m) d.step(m);
 #endif
       FST(15);
       WMARK(4);
@@ -1129,18 +1168,18 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         // head rows stay with this workgroup inside the segment (plain write-back stores); the
         // segment's last element hands them to the next segment group by group: write-through
         // stores, drained, then Ac[k][j][s][g]++ (one group later, after the next drain)
-        if (has_next) store_head_pair<B, TQR_HEAD_ST_AUX>(H, hrs, hoff + g * IB * sizeof(S));
-        else store_head_pair<B, 16>(H, hrs, hoff + g * IB * sizeof(S));
+        if (has_next) store_head_pair<B, TQR_HEAD_ST_AUX, IB>(H, hrs, hoff + g * IB * sizeof(S));
+        else store_head_pair<B, 16, IB>(H, hrs, hoff + g * IB * sizeof(S));
         FST(2);
         // the next group's head rows straight into H (its stores above have read it): a separate
         // prefetch register set was copied into H after phase 2, and that copy waited vmcnt(0) —
         // in the hand-over group for the whole streamed strip
-        if (FLOW_PF && g + 1 < NG) load_head_pair<B, TQR_HEAD_LD_AUX>(H, hrs, hoff + (g + 1) * IB * sizeof(S));
+        if (FLOW_PF && g + 1 < NG) load_head_pair<B, TQR_HEAD_LD_AUX, IB>(H, hrs, hoff + (g + 1) * IB * sizeof(S));
       }
 #endif
       FST(14);
       WMARK(5);
-      phase_prio(true);
+      phase_prio<C>(true);
       if (active) {
         if (pipe) {
           S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
@@ -1150,9 +1189,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
                                , blockIdx.x == 0 && gtr_n < GTR_GROUPS ? g_xtr + ((size_t)gtr_n * 8 + (t >> 6)) * 8 : nullptr
 #endif
           };
-          apply_x4<B, XPipe<B, S>>(Vs, X, W, xp);
+          apply_x4<B, XPipe<B, S>, IB>(Vs, X, W, xp);
         } else {
-          apply_x4<B>(Vs, X, W);
+          apply_x4<B, NoPost, IB>(Vs, X, W);
         }
       }
       if (g + 1 == NG) xin = pipe;
@@ -1186,18 +1225,20 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
 namespace tqr {
 
 // dynamic LDS (doubles) of the task paths; the LDS tail (task word, verdicts, ...) follows
-template <int B, typename S>
+template <int B, typename S, class C>
 constexpr int flow_lds_doubles() {
-  using G = Geo<B>;
+  using G = FGeo<B, C>;
   constexpr int panel = G::VSZ + 8 * G::TSZ + G::IB + 2 + 2 * 4 * 32 + 4 * 32 + 2 * 32;
-  constexpr int chain = 2 * (Img<B, S>::V + Img<B, S>::T);
+  constexpr int chain = 2 * (FImg<B, S, C>::V + FImg<B, S, C>::T);
   return panel > chain ? panel : chain;
 }
 
-template <int B, typename S>
-__global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
+template <int B, typename S, class C>
+__global__ __launch_bounds__(C::NT, C::WPC) void k_flow(FlowArgs a) {
+  static_assert(sizeof(S) == 8 || C::NW == 8, "the fp32 chain runs the 8-wave shape");
+  static_assert(C::WPC == 1 || (flow_lds_doubles<B, S, C>() * 8 + 1536) * C::WPC <= 163840, "LDS per CU");
   extern __shared__ __align__(16) double lds[];
-  int* s_task = reinterpret_cast<int*>(lds + flow_lds_doubles<B, S>());
+  int* s_task = reinterpret_cast<int*>(lds + flow_lds_doubles<B, S, C>());
   int* s_flag = s_task + 1;
 #ifdef TQR_FLOW_STAMPS
   if (threadIdx.x == 0) {
@@ -1230,15 +1271,15 @@ __global__ __launch_bounds__(FLOW_NT, 1) void k_flow(FlowArgs a) {
 #endif
     if (type == T_CHAIN) {
       if constexpr (sizeof(S) == 8)
-        flow_chain<B, S>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
+        flow_chain<B, S, C>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                          s_flag);
       else
         flow_chain32<B>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                         s_flag);
     } else if (type == T_UP || type == T_DOWN) {
-      flow_xfer<B, S>(a, type == T_UP, it.m, (it.ts >> 8) & 0xff, s_flag);
+      flow_xfer<B, S, C>(a, type == T_UP, it.m, (it.ts >> 8) & 0xff, s_flag);
     } else {
-      flow_panel<B, S>(a, type, it.l, it.k, lds, s_flag);
+      flow_panel<B, S, C>(a, type, it.l, it.k, lds, s_flag);
     }
     __syncthreads();
 #ifdef TQR_FLOW_STAMPS

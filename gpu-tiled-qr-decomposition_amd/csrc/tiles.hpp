@@ -293,11 +293,11 @@ struct NoPost {
   template <typename XA>
   __device__ __forceinline__ void fin(XA&) const {}
 };
-template <int B, bool HEAD, bool PF = true, typename Hook = NoHook, typename Post = NoPost>
+template <int B, bool HEAD, bool PF = true, typename Hook = NoHook, typename Post = NoPost, int IBX = Geo<B>::IB>
 __device__ __forceinline__ void apply_x(const double* __restrict__ Vs, double (&X)[Geo<B>::NKS],
-                                        const double (&W)[Geo<B>::NRI], int ks0, const Hook& hook = Hook(),
+                                        const double (&W)[Geo<B, IBX>::NRI], int ks0, const Hook& hook = Hook(),
                                         const Post& post = Post()) {
-  using g = Geo<B>;
+  using g = Geo<B, IBX>;
   constexpr int NRI = g::NRI, NKS = g::NKS, VP = g::VP;
   const int lane = threadIdx.x & 63, x = lane >> 4, y = lane & 3;
   // X += V W   (A operand: V[4ks+y][4wi+x]); two k-steps per region, next pair's reads ahead.
@@ -395,12 +395,12 @@ __device__ __forceinline__ void apply_x4(const double* __restrict__ Vs, double (
   post.fin(X);
 }
 
-template <int B, bool HEAD, bool PF = true, bool TPACK = false>
+template <int B, bool HEAD, bool PF = true, bool TPACK = false, int IBX = Geo<B>::IB>
 __device__ __forceinline__ void apply_group(const double* __restrict__ Vs, const double* __restrict__ Ts,
-                                            double (&X)[Geo<B>::NKS], double (&H)[Geo<B>::NRI], int ks0) {
-  double W[Geo<B>::NRI];
-  apply_zw<B, HEAD, NoHook, PF, TPACK>(Vs, Ts, X, H, W, ks0);
-  apply_x<B, HEAD, PF>(Vs, X, W, ks0);
+                                            double (&X)[Geo<B>::NKS], double (&H)[Geo<B, IBX>::NRI], int ks0) {
+  double W[Geo<B, IBX>::NRI];
+  apply_zw<B, HEAD, NoHook, PF, TPACK, false, IBX>(Vs, Ts, X, H, W, ks0);
+  apply_x<B, HEAD, PF, NoHook, NoPost, IBX>(Vs, X, W, ks0);
 }
 
 // Strip loads/stores: X[ks] <- tile(rows 4ks+x, column col0 + 4blk + y).
@@ -515,10 +515,10 @@ __device__ __forceinline__ unsigned head_off(size_t ldm, int r0) {
   const int lane = threadIdx.x & 63, x = lane >> 4, c = lane & 15;
   return (unsigned)(((size_t)c * ldm + r0 + x) * sizeof(S));
 }
-template <int B, typename S, int AUX>
-__device__ __forceinline__ void load_head_buf(double (&H)[Geo<B>::NRI], __amdgpu_buffer_rsrc_t rs, unsigned base) {
+template <int B, typename S, int AUX, int IBX = Geo<B>::IB, int NRI_ = Geo<B, IBX>::NRI>
+__device__ __forceinline__ void load_head_buf(double (&H)[NRI_], __amdgpu_buffer_rsrc_t rs, unsigned base) {
 #pragma unroll
-  for (int r = 0; r < Geo<B>::NRI; ++r) {
+  for (int r = 0; r < NRI_; ++r) {
     if constexpr (sizeof(S) == 8) {
       const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, base, 4 * r * 8, AUX);
       H[r] = __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
@@ -527,10 +527,10 @@ __device__ __forceinline__ void load_head_buf(double (&H)[Geo<B>::NRI], __amdgpu
     }
   }
 }
-template <int B, typename S, int AUX>
-__device__ __forceinline__ void store_head_buf(const double (&H)[Geo<B>::NRI], __amdgpu_buffer_rsrc_t rs, unsigned base) {
+template <int B, typename S, int AUX, int IBX = Geo<B>::IB, int NRI_ = Geo<B, IBX>::NRI>
+__device__ __forceinline__ void store_head_buf(const double (&H)[NRI_], __amdgpu_buffer_rsrc_t rs, unsigned base) {
 #pragma unroll
-  for (int r = 0; r < Geo<B>::NRI; ++r) {
+  for (int r = 0; r < NRI_; ++r) {
     if constexpr (sizeof(S) == 8) {
       const unsigned long long u = (unsigned long long)__double_as_longlong(H[r]);
       __attribute__((ext_vector_type(2))) unsigned v = {(unsigned)u, (unsigned)(u >> 32)};

@@ -41,7 +41,7 @@ __device__ __noinline__ bool column_final(const FlowArgs& a, int j, int NG) {
 // One chunk of one tile column between host memory and the device matrix: B columns of `nr`
 // elements each, 16-B accesses when both sides allow them (else element by element). UNR columns
 // at a time, KV 16-B vectors per lane and column in flight (a host read is a PCIe round trip).
-template <typename S, bool UP>
+template <typename S, bool UP, int NT>
 __device__ __forceinline__ void xfer_columns(const FlowArgs& a, int B, int j, int r0, int nr) {
   const int t = threadIdx.x;
   S* dA = (S*)a.A;
@@ -62,12 +62,12 @@ __device__ __forceinline__ void xfer_columns(const FlowArgs& a, int B, int j, in
         hr[u] = uniform_rsrc(host + ((size_t)col * hld + r0) * sizeof(S));
         dr[u] = uniform_rsrc(dA + (size_t)col * dld + r0);
       }
-      for (int v0 = 0; v0 < nv; v0 += KV * FLOW_NT) {
+      for (int v0 = 0; v0 < nv; v0 += KV * NT) {
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
 #pragma unroll
           for (int k = 0; k < KV; ++k) {
-            const int x = v0 + k * FLOW_NT + t;
+            const int x = v0 + k * NT + t;
             if (x < nv && c0 + u < B)
               v[u][k] = UP ? __builtin_amdgcn_raw_buffer_load_b128(hr[u], 16 * x, 0, XFER_AUX_HOST)
                            : __builtin_amdgcn_raw_buffer_load_b128(dr[u], 16 * x, 0, 16);
@@ -76,7 +76,7 @@ __device__ __forceinline__ void xfer_columns(const FlowArgs& a, int B, int j, in
         for (int u = 0; u < UNR; ++u)
 #pragma unroll
           for (int k = 0; k < KV; ++k) {
-            const int x = v0 + k * FLOW_NT + t;
+            const int x = v0 + k * NT + t;
             if (x < nv && c0 + u < B) {
               if (UP) __builtin_amdgcn_raw_buffer_store_b128(v[u][k], dr[u], 16 * x, 0, 16);
               else __builtin_amdgcn_raw_buffer_store_b128(v[u][k], hr[u], 16 * x, 0, XFER_AUX_HOST);
@@ -89,7 +89,7 @@ __device__ __forceinline__ void xfer_columns(const FlowArgs& a, int B, int j, in
       const int col = col0 + c;
       const __amdgpu_buffer_rsrc_t hr = uniform_rsrc(host + ((size_t)col * hld + r0) * sizeof(S));
       const __amdgpu_buffer_rsrc_t dr = uniform_rsrc(dA + (size_t)col * dld + r0);
-      for (int r = t; r < nr; r += FLOW_NT) {
+      for (int r = t; r < nr; r += NT) {
         if constexpr (sizeof(S) == 8) {
           const auto v = UP ? __builtin_amdgcn_raw_buffer_load_b64(hr, 8 * r, 0, XFER_AUX_HOST)
                             : __builtin_amdgcn_raw_buffer_load_b64(dr, 8 * r, 0, 16);
@@ -106,9 +106,9 @@ __device__ __forceinline__ void xfer_columns(const FlowArgs& a, int B, int j, in
   }
 }
 
-template <int B, typename S>
+template <int B, typename S, class C>
 __device__ __noinline__ void flow_xfer(const FlowArgs& a, bool up, int j, int c, int* sflag) {
-  constexpr int NG = Geo<B>::NG;
+  constexpr int NG = FGeo<B, C>::NG;
   const int r0 = c * a.xrows, nr = min(a.m - r0, a.xrows);
   FST(6);
   bool ok = true;
@@ -118,12 +118,12 @@ __device__ __noinline__ void flow_xfer(const FlowArgs& a, bool up, int j, int c,
   }
   if (!wg_verdict(ok, sflag)) return;
   if (up) {
-    xfer_columns<S, true>(a, B, j, r0, nr);
+    xfer_columns<S, true, C::NT>(a, B, j, r0, nr);
     wg_publish(&a.Uc[j], 1);  // sc1 stores drained, then one add
     // host-transfer progress: waits that expire while it moves keep waiting (flow.hpp timed_out)
     if (threadIdx.x == 0) __hip_atomic_fetch_add(gptr(a.err + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    xfer_columns<S, false>(a, B, j, r0, nr);
+    xfer_columns<S, false, C::NT>(a, B, j, r0, nr);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0 && a.hdn) {
