@@ -162,22 +162,24 @@ def check_output(A0, A, m, n):
     return rel
 
 
-def check_owned_columns(A0, A, m, n, b, rank, world, owned=None):
+def check_owned_columns(A0, A, m, n, b, rank, world, owned=None, packed=False):
     """The same check for one rank of a multi-GPU factorisation: every column of R lives in its
     tile column, and a tile column is finished by its owner (panel and all its updates), so each
     rank checks the columns it owns on its own device. owned: those tile columns as the plan deals
-    them (DistTiledQR.owned_cols); default the snake partition (tqr.owned_tile_cols)."""
+    them (DistTiledQR.owned_cols); default the snake partition (tqr.owned_tile_cols). packed: A0 and
+    A hold only the owned tile columns, in order (the multi-GPU storage; else full (n, m) arrays)."""
     import torch
     import tqr
     q = n // b
     if owned is None:
         owned = tqr.owned_tile_cols(q, rank, world)
     own = torch.tensor(owned, device=A.device, dtype=torch.long)
-    cols = torch.arange(n, device=A.device).view(q, b)[own].reshape(-1)
-    Ao = A[cols].double()  # (n, m) storage: row c = matrix column c
+    cols = torch.arange(n, device=A.device).view(q, b)[own].reshape(-1)  # global matrix columns
+    rows = torch.arange(len(owned) * b, device=A.device) if packed else cols  # where they are stored
+    Ao = A[rows].double()  # (n, m) storage: row c = matrix column c
     keep = torch.arange(m, device=A.device)[None, :] <= cols[:, None]  # R: rows r <= c
     nr = torch.linalg.vector_norm(Ao * keep, dim=1)
-    na = torch.linalg.vector_norm(A0[cols].double(), dim=1)
+    na = torch.linalg.vector_norm(A0[rows].double(), dim=1)
     rel = ((na - nr).abs() / na.clamp_min(1e-300)).max().item()
     tol = 1e-10 if A.dtype == torch.float64 else 1e-4
     if not rel <= tol:
@@ -351,22 +353,24 @@ def main():
             single = single_gpu_leg(tqr, torch, m, n, b, dt, args.steps, args.warmup)
         dist.barrier()
 
-    A0 = torch.empty((n, m), dtype=dt, device="cuda")
-    tqr.fill_randzo(A0, m, n, 5)
+    if world == 1:
+        plan = tqr.TiledQR(m, n, b, dt)
+        A0 = torch.empty((n, m), dtype=dt, device="cuda")
+        tqr.fill_randzo(A0, m, n, 5)
+        tau = torch.zeros((min(m, n) // b, m), dtype=dt, device="cuda")
+    else:
+        # a rank stores only its own tile columns (packed, include/tqr.h "multi-GPU"): its share of
+        # the same global RANDZO matrix, generated in place
+        plan = tqr.DistTiledQR(m, n, b, dt)
+        A0, tau = plan.alloc_local()
+        plan.fill_randzo_local(A0, 5)
     A = torch.empty_like(A0)
     A.copy_(A0)
-    tau = torch.zeros((min(m, n) // b, m), dtype=dt, device="cuda")
-    plan = tqr.TiledQR(m, n, b, dt) if world == 1 else tqr.DistTiledQR(m, n, b, dt)
     stream = torch.cuda.current_stream().cuda_stream
-    # this rank's tile columns (all of them at N = 1; DistTiledQR's snake partition otherwise):
-    # rows j*b..j*b+b-1 of the (n, m) array
-    own_cols = None if world == 1 else torch.tensor(plan.owned_cols(), device=A.device, dtype=torch.long)
+    local_bytes = A0.numel() * A0.element_size()
 
     def step():
-        if own_cols is None:
-            A.copy_(A0)
-        else:
-            A.view(q, b, m)[own_cols] = A0.view(q, b, m)[own_cols]
+        A.copy_(A0)
         plan.execute(A, tau, stream=stream)
 
     # The factorisation is in place, so every timed step needs a fresh input: when HBM allows, one
@@ -420,7 +424,7 @@ def main():
         ok_rel = check_output(A0, Afin, m, n)
     else:
         try:
-            ok_rel = check_owned_columns(A0, Afin, m, n, b, rank, world, plan.owned_cols())
+            ok_rel = check_owned_columns(A0, Afin, m, n, b, rank, world, plan.owned_cols(), packed=True)
         except RuntimeError as e:
             ok_rel = None
             if rank_status == "ok":
@@ -431,7 +435,9 @@ def main():
     if dist:
         # per rank: engine status, forwarded bytes, and with a stamps build
         # (TQR_LIB=libtqr_fst.so) the share of workgroup time the panels spent forwarding
-        mine = {"rank": rank, "status": rank_status, "fwd_bytes": plan.fwd_bytes(), "column_norm_rel_err": ok_rel}
+        mine = {"rank": rank, "status": rank_status, "fwd_bytes": plan.fwd_bytes(), "column_norm_rel_err": ok_rel,
+                "tile_cols": plan.local_cols(), "matrix_bytes": local_bytes,
+                "hbm_in_use_bytes": torch.cuda.memory_allocated()}
         L = tqr.lib()
         if hasattr(L, "tqr_debug_flow_stamps"):
             import ctypes

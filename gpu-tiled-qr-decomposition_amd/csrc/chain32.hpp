@@ -264,7 +264,8 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
   const int t = threadIdx.x, w = t >> 6;
   const int col = s * FLOW_SW + 16 * w;
   const bool active = B % FLOW_SW == 0 || col < B;
-  float* At = A + (size_t)j * B * ldm + (size_t)k * B;
+  float* const Aj = uni(A + (size_t)(j / uni(a.cdiv)) * B * ldm);  // tile column j (FlowArgs::cdiv)
+  float* At = Aj + (size_t)k * B;
   double* const wk = uni(a.Wk[k]);
   const int P = uni(a.p), Q = uni(a.q), NS = uni(a.ns);
   int* const err = uni(a.err);
@@ -292,12 +293,13 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
   bool xin = false;  // this element's strip was loaded during the previous element's last phase 2
   const bool remote = a.dist && tile_owner(k, a.world, a.cyclic) != a.rank;
   int* const rf = uni(a.Rf + (size_t)k * P * NG);
+  const int ep = uni(a.epoch);
   int fl_pf = -1;  // index (i * NG + g) of the flag the early load in fls is of
   auto ready = [&](int i_, int g_) -> bool {
     if (!remote) return pv.ensure(rc, g_, i_ - k + 1, err, false);
     const int fi = i_ * NG + g_;
-    if (fi == fl_pf && lds_ld_volatile(fls) >= 1) return true;
-    return spin_ge_i(rf + fi, 1, err, true);
+    if (fi == fl_pf && lds_ld_volatile(fls) >= ep) return true;
+    return spin_ge_i(rf + fi, ep, err, true);
   };
   const Strip32<B> hs(At, ldm, col);  // the head tile's strip
   FST(6);
@@ -323,7 +325,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
       if (!sync_point<false, true>(ok, sflag, par)) return;
     }
     FST(7);
-    float* Xt = ts ? A + (size_t)j * B * ldm + (size_t)i * B : At;
+    float* Xt = ts ? Aj + (size_t)i * B : At;
     if (!dma_next) {
       DmaJob<B, float, ShapeW8> d{lds + buf * BUF, vimg(i, 0), timg(i, 0), sflag};
       for (int m = 0; m < DmaJob<B, float, ShapeW8>::STEPS; ++m) d.step(m);
@@ -435,7 +437,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
 #pragma unroll
               for (int mi = 0; mi < NMI; ++mi) Hd[NMI + mi] = ld_f4(hs.rs, hs.off((g + 1) * NMI + mi));
             if (pipe) {
-              float* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
+              float* Xn = Aj + (size_t)inext * B;
               const XPipe32<B> xp{xs.rs, uniform_rsrc(Xn + (size_t)col * ldm), xs.base};
               apply32<B, true>(VRp, TPi, X, Hd, dh, xp);
             } else {

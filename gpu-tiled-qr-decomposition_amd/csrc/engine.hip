@@ -280,12 +280,15 @@ __global__ __launch_bounds__(NT, 1) void k_build_t(Args a) {
 }
 
 // RANDZO-distributed synthetic input: ((h mod 201) - 100) / 100 from a splitmix64 hash.
+// col0: the first column's index in the global matrix (the value of element (i, j) depends only on
+// the seed and its global position, so a rank can fill just its own columns)
 template <typename S>
-__global__ void k_randzo(S* A, int m, int n, long ldm, unsigned long long seed) {
+__global__ void k_randzo(S* A, int m, int n, long ldm, unsigned long long seed, long col0) {
   long total = (long)m * n;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     long jj = e / m, ii = e % m;
-    unsigned long long z = seed * 0x9E3779B97F4A7C15ull + (unsigned long long)e + 0x632BE59BD9B4E019ull;
+    const unsigned long long eg = (unsigned long long)(e + col0 * m);  // global element index
+    unsigned long long z = seed * 0x9E3779B97F4A7C15ull + eg + 0x632BE59BD9B4E019ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     z ^= z >> 31;
@@ -744,7 +747,8 @@ struct tqr_plan {
   // multi-GPU (tile-column snake partition; cyclic = TQR_DIST_PART=cyclic): rank / world, uncached
   // panel counters, forward counters, peer workspaces opened by IPC
   int rank = 0, world = 1, cyclic = 0;
-  int* d_rf = nullptr;     // multi-GPU member flags (uncached), kmax x p x ng
+  int* d_rf = nullptr;     // multi-GPU member flags (uncached), kmax x p x ng, then Done[world]
+  int epoch = 0;           // multi-GPU: launches so far (the member flags' and Done's values)
   PeerBufs* d_peers = nullptr;
   double** d_peer_wk = nullptr;  // world x kmax opened peer workspace pointers
   std::vector<void*> opened;     // IPC-opened peer pointers
@@ -954,8 +958,8 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
-    // next, err, host-transfer progress (flow.hpp timed_out), Rc, Tc, Ac, Rt, Rr, then Uc (upload chunks per tile column, host-pointer API)
-    pl->sync_ints = 3 + 3 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns +
+    // next, err, host-transfer progress (flow.hpp timed_out), exit count, Rc, Tc, Ac, Rt, Rr, then Uc (upload chunks per tile column, host-pointer API)
+    pl->sync_ints = 4 + 3 * (size_t)pl->kmax * pl->ng + (size_t)pl->p * pl->q * pl->ns +
                     (size_t)pl->kmax * pl->q * pl->ns * pl->ng + (size_t)pl->q;
     if (pl->nflow <= 0 || hipMalloc(&pl->d_flow, sizeof(Item) * pl->nflow) != hipSuccess ||
         hipMalloc(&pl->d_sync, sizeof(int) * pl->sync_ints) != hipSuccess ||
@@ -984,9 +988,10 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
       tqr_plan_destroy(pl); return TQR_EHIP;
     }
     if (world > 1) {
-      // member flags in uncached memory (peers' forward tasks set them over xGMI)
-      const size_t nrf = sizeof(int) * (size_t)pl->kmax * pl->p * pl->ng;
-      if (hipExtMallocWithFlags((void**)&pl->d_rf, nrf, hipDeviceMallocUncached) != hipSuccess ||
+      // member flags (+ Done[world]) in uncached memory (peers' panels set them over xGMI); zeroed
+      // once: their values are launch epochs (flow.hpp FlowArgs)
+      const size_t nrf = sizeof(int) * ((size_t)pl->kmax * pl->p * pl->ng + world);
+      if (hipExtMallocWithFlags((void**)&pl->d_rf, nrf, hipDeviceMallocUncached) != hipSuccess || hipMemset(pl->d_rf, 0, nrf) != hipSuccess ||
           hipMalloc(&pl->d_peers, sizeof(PeerBufs) * world) != hipSuccess ||
           hipMalloc(&pl->d_peer_wk, sizeof(double*) * (size_t)world * pl->kmax) != hipSuccess) {
         tqr_plan_destroy(pl); return TQR_ENOMEM;
@@ -1120,14 +1125,20 @@ int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
   return TQR_OK;
 }
 
+// Kept for the API: since round 4 every execute resets its own (local) counters, and the
+// cross-rank flags carry launch epochs, so consecutive multi-GPU executes need no reset, host
+// synchronisation or barrier (flow.hpp FlowArgs Done[]).
 int tqr_dist_reset(tqr_plan* pl, void* stream) {
+  (void)stream;
   if (!pl || pl->world < 2) return TQR_EINVAL;
-  hipStream_t cs = (hipStream_t)stream;
-  std::lock_guard<std::mutex> lk(pl->mu);
-  HIPCHK(hipStreamWaitEvent(cs, pl->evDone, 0));
-  HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
-  HIPCHK(hipMemsetAsync(pl->d_rf, 0, sizeof(int) * (size_t)pl->kmax * pl->p * pl->ng, cs));
   return TQR_OK;
+}
+
+int tqr_dist_local_cols(const tqr_plan* pl) {
+  if (!pl) return TQR_EINVAL;
+  int c = 0;
+  for (int j = 0; j < pl->q; ++j) c += tile_owner(j, pl->world, pl->cyclic) == pl->rank;
+  return c;
 }
 
 long long tqr_plan_fwd_bytes(const tqr_plan* pl) {
@@ -1288,12 +1299,15 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     f.tasks = xa ? pl->d_flow_x : pl->d_flow;
     f.ntasks = xa ? pl->nflow_x : pl->nflow;
     f.m = pl->m; f.p = pl->p; f.q = pl->q; f.kmax = pl->kmax; f.ns = pl->ns;
-    f.next = pl->d_sync; f.err = pl->d_sync + 1; f.Rc = pl->d_sync + 3;
+    f.next = pl->d_sync; f.err = pl->d_sync + 1; f.exitc = pl->d_sync + 3; f.Rc = pl->d_sync + 4;
     f.Tc = f.Rc + (size_t)pl->kmax * pl->ng;
     f.Ac = f.Tc + (size_t)pl->p * pl->q * pl->ns;
     f.Rt = f.Ac + (size_t)pl->kmax * pl->q * pl->ns * pl->ng;
     f.Rr = f.Rt + (size_t)pl->kmax * pl->ng;
     f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.cyclic = pl->cyclic; f.peers = pl->d_peers; f.Rf = pl->d_rf;
+    f.cdiv = pl->world;  // multi-GPU: the rank's own tile columns only, packed (FlowArgs::cdiv)
+    f.rf_done = (long)pl->kmax * pl->p * pl->ng;
+    f.epoch = pl->world > 1 ? ++pl->epoch : 0;
     f.seglen = pl->knobs.seglen; f.seglen_la = pl->knobs.seglen_la; f.la_tail = pl->knobs.la_tail;
     if (xa) {
       f.hsrc = xa->hsrc; f.hdst = xa->hdst; f.hld = xa->hld; f.hup = xa->hup; f.hdn = xa->hdn; f.gen = xa->gen;
@@ -1303,8 +1317,8 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
       f.hsrc = nullptr; f.hdst = nullptr; f.hld = 0; f.hup = nullptr; f.hdn = nullptr; f.gen = 0;
       f.Uc = nullptr; f.nxc = 0; f.xrows = 0;
     }
-    // multi-GPU: counters and flags are reset by tqr_dist_reset (all ranks, then a barrier)
-    if (pl->world == 1) HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
+    // local progress counters (multi-GPU: the member flags are epoch-valued and never reset)
+    HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
     if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
     hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(pl->nt), pl->ldsF, cs, f);
     HIPCHK(hipGetLastError());
@@ -1811,16 +1825,19 @@ int tqr_cache_clear(void) {
   return st;
 }
 
-int tqr_fill_randzo(int dtype, void* dA, int m, int n, int ldda, unsigned long long seed, void* stream) {
-  if (!dA || ldda < m || m <= 0 || n <= 0) return TQR_EINVAL;
-  long total = (long)m * n;
+int tqr_fill_randzo_cols(int dtype, void* dA, int m, int ncols, int ldda, unsigned long long seed, long col0, void* stream) {
+  if (!dA || ldda < m || m <= 0 || ncols <= 0 || col0 < 0) return TQR_EINVAL;
+  long total = (long)m * ncols;
   int blocks = (int)std::min<long>(65536, (total + 255) / 256);
   if (dtype == TQR_F64)
-    hipLaunchKernelGGL(k_randzo<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (double*)dA, m, n, (long)ldda, seed);
+    hipLaunchKernelGGL(k_randzo<double>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (double*)dA, m, ncols, (long)ldda, seed, col0);
   else
-    hipLaunchKernelGGL(k_randzo<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (float*)dA, m, n, (long)ldda, seed);
+    hipLaunchKernelGGL(k_randzo<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (float*)dA, m, ncols, (long)ldda, seed, col0);
   HIPCHK(hipGetLastError());
   return TQR_OK;
+}
+int tqr_fill_randzo(int dtype, void* dA, int m, int n, int ldda, unsigned long long seed, void* stream) {
+  return tqr_fill_randzo_cols(dtype, dA, m, n, ldda, seed, 0, stream);
 }
 
 }  // extern "C"

@@ -207,12 +207,20 @@ struct FlowArgs {
   int* Ac;
   int* Rt;
   int* Rr;
-  // multi-GPU: dist = world > 1. Rf[k][i][g] (uncached memory) = 1 once the owner of panel k
-  // forwarded the V/T images of member i, group g into this rank's workspace (set by the peer
-  // over xGMI, polled at system scope). Panel counters Rc/Rr/Rt stay local to the owner.
+  // multi-GPU: dist = world > 1. Rf[k][i][g] (uncached memory) = the epoch of the launch whose
+  // owner of panel k forwarded the V/T images of member i, group g into this rank's workspace
+  // (set by the peer over xGMI, polled at system scope; never reset: a launch waits for its own
+  // epoch). Panel counters Rc/Rr/Rt stay local to the owner. Rf + rf_done: Done[r] = the last
+  // epoch rank r's launch completed (every rank writes its own entry into every peer's array at
+  // the end of its launch); a panel task forwards into peer r's workspace only once Done[r] has
+  // reached epoch - 1 (peer r no longer reads the previous launch's images) — so consecutive
+  // launches need no host synchronisation or barrier between the ranks.
   int dist, rank, world, cyclic;  // cyclic: TQR_DIST_PART=cyclic diagnostic partition (j % world)
   const PeerBufs* peers;
   int* Rf;
+  int epoch;
+  long rf_done;  // offset of Done[] in Rf
+  int* exitc;    // workgroups that left the task loop (local, zeroed per launch)
   // host-pointer API (xfer.hpp; all null / 0 on the device API): the launch uploads its input
   // from hsrc and downloads its result to hdst (host memory, leading dimension hld) in chunks of
   // xrows rows, nxc per tile column. hup[j] >= gen: the host staged column j (null: hsrc was
@@ -226,6 +234,11 @@ struct FlowArgs {
   int* hdn;
   int* Uc;
   int gen, nxc, xrows, seglen, seglen_la, la_tail;
+  // storage of the tile columns: global tile column j is local column j / cdiv of A (and tau
+  // column k of panel k local column k / cdiv). Single GPU: cdiv = 1. Multi-GPU: cdiv = world —
+  // a rank stores only the tile columns it owns (one per block of `world` consecutive columns,
+  // in the snake and the cyclic partition alike), packed in column order.
+  int cdiv;
 };
 
 // Multi-GPU owner of tile column j (its panel and all its updates): "snake" order over the ranks
@@ -676,7 +689,7 @@ __device__ __noinline__ void panel_idle(const FwdJob* fjp, int IB, bool TS) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (int r = 0; r < a.world; ++r)
       if (r != a.rank)
-        __hip_atomic_store((int*)peer(pf, r) + fj.fo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store((int*)peer(pf, r) + fj.fo, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -697,9 +710,11 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
   S* tau = (S*)a.tau;
   const size_t ldm = a.ldm;
   const int t = threadIdx.x, w = t >> 6;
-  S* Rt = A + (size_t)k * B * ldm + (size_t)k * B;
+  // tile column k and tau column k in this rank's storage (FlowArgs::cdiv)
+  const int kl = k / a.cdiv;
+  S* Rt = A + (size_t)kl * B * ldm + (size_t)k * B;
   const bool qrs = type == QRS;
-  S* Bt = qrs ? Rt : A + (size_t)k * B * ldm + (size_t)l * B;
+  S* Bt = qrs ? Rt : A + (size_t)kl * B * ldm + (size_t)l * B;
   const int pos = qrs ? 0 : l - k;  // position in the panel chain
   FST(6);
   // the tile(s) must have received step k-1 on every strip (step 0, host-pointer API: tile
@@ -716,6 +731,13 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
   double H[G::NRI];
   const int me = qrs ? k : l;
   if (a.dist && t == 0) *lds_int(sflag + 36) = 0;  // the forwarding waves' arrival counter
+  if (a.dist) {  // every peer has finished the previous launch (it reads no more of its images)
+    bool ok = true;
+    if (t == FLOW_PT)
+      for (int r = 0; r < a.world && ok; ++r)
+        if (r != a.rank) ok = spin_ge(a.Rf + a.rf_done + r, a.epoch - 1, a.err, true);
+    if (!wg_verdict(ok, sflag)) return;
+  }
   for (int g = 0; g < NG; ++g) {
     const int c0 = g * IB;
     if (!qrs) {  // R_kk rows of group g as left by the previous chain member
@@ -773,7 +795,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
         if (r <= c) st(Rt + (size_t)(c0 + c) * ldm + c0 + r, Hs[r * TP + c]);
       }
     }
-    if (t < IB) st(tau + (size_t)k * a.m + (size_t)(qrs ? k : l) * B + c0 + t, tauv[t]);
+    if (t < IB) st(tau + (size_t)kl * a.m + (size_t)(qrs ? k : l) * B + c0 + t, tauv[t]);
     wg_publish(&a.Rr[(size_t)k * NG + g], 1);  // includes the drain and the barrier
     if (qrs) {
       for (int idx = t; idx < B * IB; idx += NT) {
@@ -863,7 +885,7 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const size_t fo = ((size_t)k * a.p + me) * NG + g;
       for (int r = 0; r < a.world; ++r)
-        if (r != a.rank) __hip_atomic_store(&a.peers[r].Rf[fo], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (r != a.rank) __hip_atomic_store(&a.peers[r].Rf[fo], a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     FST(23);
   }
@@ -965,7 +987,9 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   // element start behind an s_waitcnt vmcnt(0) (a full drain of the previous hand-over)
   const size_t colo = uni64((size_t)col * ldm);
   const bool active = B % SW == 0 || col < B;  // (compile-time true unless B < SW)
-  S* At = A + (size_t)j * B * ldm + (size_t)k * B;  // tile (k,j): the chain's head rows
+  // tile column j in this rank's storage (FlowArgs::cdiv)
+  S* const Aj = uni(A + (size_t)(j / uni(a.cdiv)) * B * ldm);
+  S* At = Aj + (size_t)k * B;  // tile (k,j): the chain's head rows
   // everything the group loop needs from FlowArgs, read once per task: the asm memory clobbers
   // of the sync points would otherwise force a reload per group — for Wk[k] a global load whose
   // latency sat in front of the group's first LDS-DMA
@@ -1001,12 +1025,13 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
   // multi-GPU, panel owned by another rank: per-member flags forwarded by the owner
   const bool remote = a.dist && tile_owner(k, a.world, a.cyclic) != a.rank;
   int* const rf = uni(a.Rf + (size_t)k * P * NG);
+  const int ep = uni(a.epoch);
   int fl_pf = -1;  // poll thread: index (i * NG + g) of the flag the early load in fls is of
   auto ready = [&](int i_, int g_) -> bool {
     if (!remote) return pv.ensure(rc, g_, i_ - k + 1, err, false);
     const int fi = i_ * NG + g_;
-    if (fi == fl_pf && lds_ld_volatile(fls) >= 1) return true;
-    return spin_ge_i(rf + fi, 1, err, true);
+    if (fi == fl_pf && lds_ld_volatile(fls) >= ep) return true;
+    return spin_ge_i(rf + fi, ep, err, true);
   };
   FST(6);
   if (k == 0 && a.Uc) {  // host-pointer API: tile column j uploaded (xfer.hpp)
@@ -1031,7 +1056,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       if (!sync_point<false, false, PT>(ok, sflag, par)) return;
     }
     FST(7);
-    S* Xt = ts ? A + (size_t)j * B * ldm + (size_t)i * B : At;
+    S* Xt = ts ? Aj + (size_t)i * B : At;
     if (!dma_next) {  // (first: the strip and head loads must be the youngest, see sync_point_first)
       Dma d{lds + buf * BUF, vimg(i, 0), timg(i, 0), sflag};
       for (int m = 0; m < Dma::STEPS; ++m) d.step(m);
@@ -1182,7 +1207,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
       phase_prio<C>(true);
       if (active) {
         if (pipe) {
-          S* Xn = A + (size_t)j * B * ldm + (size_t)inext * B;
+          S* Xn = Aj + (size_t)inext * B;
           const XPipe<B, S> xp{uniform_rsrc(Xt + colo), uniform_rsrc(Xn + colo),
                                (unsigned)((((size_t)(t & 15)) * ldm + 2 * ((t & 63) >> 4)) * sizeof(S))
 #ifdef TQR_FLOW_STAMPS
@@ -1285,6 +1310,20 @@ __global__ __launch_bounds__(C::NT, C::WPC) void k_flow(FlowArgs a) {
 #ifdef TQR_FLOW_STAMPS
     if (threadIdx.x == 0 && idx < (1 << 18)) g_ttl[3 * idx + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
+  }
+  // multi-GPU: the last workgroup out tells every rank (itself included) that this launch is done
+  // (flow.hpp FlowArgs Done[]): every workgroup's memory operations are complete before it counts
+  // itself out, so no read of the workspaces is outstanding when the peers may write them again
+  if (a.dist) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(gptr(a.exitc), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int r = 0; r < a.world; ++r)
+        __hip_atomic_store(a.peers[r].Rf + a.rf_done + a.rank, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 #ifdef TQR_FLOW_STAMPS
   FST(6);

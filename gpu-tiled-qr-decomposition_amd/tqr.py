@@ -73,6 +73,8 @@ def lib():
     L.tqr_plan_stats.argtypes = [_P, ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(_I), ctypes.POINTER(ctypes.c_double)]
     L.tqr_fill_randzo.argtypes = [_I, _P, _I, _I, _I, ctypes.c_ulonglong, _P]
+    L.tqr_fill_randzo_cols.argtypes = [_I, _P, _I, _I, _I, ctypes.c_ulonglong, ctypes.c_long, _P]
+    L.tqr_dist_local_cols.argtypes = [_P]
     for nm in ("tqr_tile_geqrt", "tqr_tile_unmqr", "tqr_tile_tsqrt", "tqr_tile_tsmqr"):
         getattr(L, nm).restype = _I
     L.tqr_dist_plan_create.argtypes = [ctypes.POINTER(_P), _I, _I, _I, _I, _I, _I]
@@ -198,12 +200,13 @@ def owned_tile_cols(q, rank, world):
 
 
 class DistTiledQR(TiledQR):
-    """One rank's share of a multi-GPU factorisation (tile-column cyclic partition, one process
-    per GPU; include/tqr.h "multi-GPU"). Tile column j belongs to rank tile_owner(j, world) (snake
-    order 0..W-1, W-1..0, ...). The handle
-    exchange and the per-factorisation barrier go over torch.distributed (`group`); the panel
-    data moves GPU to GPU inside the persistent launch (xGMI stores into IPC-opened peer
-    workspaces), not through the collective library."""
+    """One rank's share of a multi-GPU factorisation (tile-column partition, one process per GPU;
+    include/tqr.h "multi-GPU"). Tile column j belongs to rank owner(j) (snake order 0..W-1,
+    W-1..0, ...), and a rank stores only its own tile columns, packed: global tile column j is
+    local tile column j // W (alloc_local / fill_randzo_local). The handle exchange goes over
+    torch.distributed (`group`) once; the panel data moves GPU to GPU inside the persistent
+    launch (xGMI stores into IPC-opened peer workspaces), and consecutive executes need no host
+    synchronisation or barrier (epoch-valued flags on the device)."""
 
     def __init__(self, m, n, b, dtype, group=None):
         import torch.distributed as dist
@@ -261,20 +264,42 @@ class DistTiledQR(TiledQR):
     def owns(self, tile_col):
         return self.owner(tile_col) == self.rank
 
+    def local_cols(self):
+        """Number of tile columns this rank stores (tqr_dist_local_cols)."""
+        c = lib().tqr_dist_local_cols(self.h)
+        if c < 0:
+            check(c, "tqr_dist_local_cols")
+        return c
+
+    def local_index(self, tile_col):
+        """Local tile column of an owned global tile column."""
+        return tile_col // self.world
+
+    def alloc_local(self, device="cuda"):
+        """(A, tau) device arrays of this rank's storage: A (local_cols * b, m) — row c = local
+        matrix column c — and the compact tau (local_cols, m)."""
+        import torch
+        dt = torch.float64 if self.dtype == TQR_F64 else torch.float32
+        nl = self.local_cols()
+        return (torch.empty((nl * self.b, self.m), dtype=dt, device=device),
+                torch.zeros((nl, self.m), dtype=dt, device=device))
+
+    def fill_randzo_local(self, A, seed, stream=None):
+        """This rank's tile columns of the global RANDZO matrix (tqr_fill_randzo_cols)."""
+        b = self.b
+        for j in self.owned_cols():
+            lj = self.local_index(j)
+            fill_randzo(A[lj * b:(lj + 1) * b], self.m, b, seed, stream=stream, col0=j * b)
+
     def fwd_bytes(self):
         """Bytes this rank forwards to its peers per factorisation (panel V/T images over xGMI)."""
         lib().tqr_plan_fwd_bytes.restype = ctypes.c_longlong
         return int(lib().tqr_plan_fwd_bytes(self.h))
 
     def execute(self, A, tau, ldda=None, stream=None):
-        """Reset this rank's counters, barrier over all ranks, launch (stream-ordered)."""
-        import torch
-        import torch.distributed as dist
+        """Launch (stream-ordered) on this rank's packed storage (alloc_local). Every rank calls it
+        the same number of times; no host synchronisation or barrier is needed between calls."""
         ldda = ldda or self.m
-        if self.world > 1:
-            check(lib().tqr_dist_reset(self.h, _P(stream or 0)), "tqr_dist_reset")
-            torch.cuda.synchronize()
-            dist.barrier(group=self.group)
         check(lib().tqr_plan_execute(self.h, _ptr(A), ldda, _ptr(tau), _P(stream or 0)), "tqr_plan_execute")
 
 
@@ -287,9 +312,10 @@ def dist_plan_check(M, N, b, rank, world, seglen=8):
     return nt.value, nf.value
 
 
-def fill_randzo(A, m, n, seed, ldda=None, stream=None):
-    check(lib().tqr_fill_randzo(_dtype_code(A.dtype), _ptr(A), m, n, ldda or m, seed, _P(stream or 0)),
-          "tqr_fill_randzo")
+def fill_randzo(A, m, n, seed, ldda=None, stream=None, col0=0):
+    """RANDZO input on the device (columns col0 .. col0 + n - 1 of the global matrix)."""
+    check(lib().tqr_fill_randzo_cols(_dtype_code(A.dtype), _ptr(A), m, n, ldda or m, seed, col0, _P(stream or 0)),
+          "tqr_fill_randzo_cols")
 
 
 def geqrt_host(A, b, with_tau=True, m=None, tau=None):

@@ -109,12 +109,18 @@ long tqr_total_tasks(int m, int n, int b);
 /* ---- multi-GPU: tile-column partition, one process per GPU ---------------------------------
  * Rank r owns the tile columns j with tqr_dist_owner(j) == r — snake order over the ranks
  * (0..W-1, W-1..0, 0..W-1, ...: every rank's columns sum to the same index total, balancing the
- * chain work that grows with j) — and factors them in a full-size matrix of
- * its own (only its columns are valid at the end; tau column k lives on the owner of column k). The
- * owner of panel k forwards each finished reflector group's V/T images to every peer over
+ * chain work that grows with j); the owner of column j factors it entirely (its panel when j <
+ * kmax, and all its updates).
+ * Storage (round 4): a rank holds ONLY its own tile columns, packed in column order — global tile
+ * column j is local tile column j / W of the rank's dA (b * tqr_dist_local_cols(plan) columns,
+ * leading dimension ldda >= m), and the taus of panel k are column k / W of its compact tau (m x
+ * tqr_dist_local_cols(plan)). A 65536 x 16384 fp64 matrix on 8 ranks is 1 GiB per rank.
+ * The owner of panel k forwards each finished reflector group's V/T images to every peer over
  * xGMI inside the persistent launch (peer workspaces opened by IPC), so panels of successive
- * steps overlap across GPUs exactly as on one GPU. Sequence per factorisation, every rank:
- *   tqr_dist_reset(plan, s); sync; <barrier over ranks>; tqr_plan_execute(plan, ...);
+ * steps overlap across GPUs exactly as on one GPU. Every rank calls tqr_plan_execute the same
+ * number of times; consecutive executes need no host synchronisation or barrier between the
+ * ranks (the cross-rank flags carry launch epochs, and a rank forwards into a peer only once that
+ * peer's previous launch has finished, all on the device).
  * Setup once: tqr_dist_export -> exchange all ranks' handle blocks (e.g. an all-gather over
  * torch.distributed / MPI) -> tqr_dist_import(plan, blocks of rank 0..world-1). */
 int tqr_dist_plan_create(tqr_plan** plan, int m, int n, int b, int dtype, int rank, int world);
@@ -123,8 +129,11 @@ int tqr_dist_plan_create(tqr_plan** plan, int m, int n, int b, int dtype, int ra
 size_t tqr_dist_handle_bytes(const tqr_plan* plan);
 int tqr_dist_export(tqr_plan* plan, void* handles, size_t len);
 int tqr_dist_import(tqr_plan* plan, const void* all_handles, size_t len);
+/* no-op since round 4 (executes reset their own counters); kept for source compatibility */
 int tqr_dist_reset(tqr_plan* plan, void* stream);
 int tqr_dist_owner(const tqr_plan* plan, int tile_col);
+/* number of tile columns this rank stores (and of its compact tau columns) */
+int tqr_dist_local_cols(const tqr_plan* plan);
 /* bytes this rank forwards to its peers per factorisation (every owned panel member's V/T images,
  * all reflector groups, to each of the world - 1 peers); 0 for a single-GPU plan */
 long long tqr_plan_fwd_bytes(const tqr_plan* plan);
@@ -184,6 +193,8 @@ int tqr_tile_batch(int dtype, int type, int b, int nblocks, const void* V, int l
 /* Device-side synthetic input with the reference's RANDZO distribution
  * ((r mod 201) - 100)/100 (qrdecomp.c:1383), from a counter-based hash of (seed, i, j). */
 int tqr_fill_randzo(int dtype, void* dA, int m, int n, int ldda, unsigned long long seed, void* stream);
+/* columns col0 .. col0 + ncols - 1 of that matrix only (a multi-GPU rank's own tile columns) */
+int tqr_fill_randzo_cols(int dtype, void* dA, int m, int ncols, int ldda, unsigned long long seed, long col0, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,10 +1,12 @@
 """Multi-GPU parity worker (launched by tests/test_dist.py under torch.distributed.run).
 
-Every rank factorises the same RANDZO matrix with the tile-column partitioned engine
-(tqr.DistTiledQR); rank 0 also factorises it alone (tqr.TiledQR, the single-GPU engine). The
-owned tile columns and taus of all ranks are gathered to rank 0 (gloo, host tensors) and
-compared with the single-GPU result: the per-tile operation sequence is identical, so the
-results must agree bit for bit. Runs the factorisation twice (counter reset / re-launch path).
+Every rank factorises its share of the same RANDZO matrix with the tile-column partitioned engine
+(tqr.DistTiledQR; each rank stores only its own tile columns, packed, generated in place from the
+global matrix's seed); rank 0 also factorises the whole matrix alone (tqr.TiledQR, the single-GPU
+engine). The owned tile columns and taus of all ranks are gathered to rank 0 (gloo, host tensors)
+and compared with the single-GPU result: the per-tile operation sequence is identical, so the
+results must agree bit for bit. Runs the factorisation twice, back to back with no host
+synchronisation between the ranks (the epoch-valued flags of consecutive launches).
 Prints one JSON line on rank 0. Usage: dist_worker.py m n b f64|f32 [device] [gather|checksum]
 
 mode "checksum" (BASELINE-size shapes, e.g. 65536 x 16384): instead of gathering the matrix,
@@ -44,39 +46,60 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     q, kmax = n // b, min(m, n) // b
-    A0 = torch.empty((n, m), dtype=dt, device="cuda")
-    tqr.fill_randzo(A0, m, n, 5)
+    plan = tqr.DistTiledQR(m, n, b, dt)
+    L0, _ = plan.alloc_local()
+    plan.fill_randzo_local(L0, 5)
+    own = plan.owned_cols()
     torch.cuda.synchronize()
     if os.environ.get("TQR_DIST_VERBOSE") == "1":
-        print(f"[rank {rank}] input ready", file=sys.stderr, flush=True)
-    plan = tqr.DistTiledQR(m, n, b, dt)
-    out = {}
+        print(f"[rank {rank}] input ready ({len(own)} tile columns, {L0.numel() * L0.element_size() >> 20} MiB)",
+              file=sys.stderr, flush=True)
+    out = {"local_cols": plan.local_cols(), "owned": len(own)}
+
+    def full_input():
+        A0 = torch.empty((n, m), dtype=dt, device="cuda")
+        tqr.fill_randzo(A0, m, n, 5)
+        return A0
+
+    # the packed local input is exactly the owned columns of the global matrix
+    if mode == "gather":
+        A0 = full_input()
+        if not all(bool(torch.equal(L0[plan.local_index(j) * b:(plan.local_index(j) + 1) * b], A0[j * b:(j + 1) * b]))
+                   for j in own):
+            raise SystemExit(f"rank {rank}: the packed local input differs from the global matrix's columns")
+        del A0
     verbose = os.environ.get("TQR_DIST_VERBOSE") == "1"
 
     def say(msg):
         if verbose:
             print(f"[rank {rank}] {msg}", file=sys.stderr, flush=True)
 
+    # two launches back to back (stream-ordered, no host synchronisation in between), then the checks
+    As, taus = [], []
     for rep in range(2):
-        A = A0.clone()
-        tau = torch.zeros((kmax, m), dtype=dt, device="cuda")
+        A, tau = plan.alloc_local()
+        A.copy_(L0)
+        As.append(A)
+        taus.append(tau)
+    for rep in range(2):
         say(f"run {rep}: execute")
-        plan.execute(A, tau)
-        say(f"run {rep}: launched")
+        plan.execute(As[rep], taus[rep])
+    for rep in range(2):
+        A, tau = As[rep], taus[rep]
         plan.status()
         say(f"run {rep}: done")
-        own = [j for j in range(q) if plan.owns(j)]
+        lc = lambda j: slice(plan.local_index(j) * b, (plan.local_index(j) + 1) * b)  # noqa: E731
+        own_tau = [k for k in range(kmax) if plan.owns(k)]
         if mode == "checksum":
-            own_tau = [k for k in range(kmax) if plan.owns(k)]
-            mine = dict(zip(own, checksums([A[j * b:(j + 1) * b] for j in own])))
-            mine_tau = dict(zip(own_tau, checksums([tau[k] for k in own_tau])))
+            mine = dict(zip(own, checksums([A[lc(j)] for j in own])))
+            mine_tau = dict(zip(own_tau, checksums([tau[plan.local_index(k)] for k in own_tau])))
             del A, tau
             allcs = [None] * world
             dist.all_gather_object(allcs, (mine, mine_tau))
             say(f"run {rep}: checksums gathered")
             if rank == 0:
                 ref = tqr.TiledQR(m, n, b, dt)
-                R = A0.clone()
+                R = full_input()
                 rtau = torch.zeros((kmax, m), dtype=dt, device="cuda")
                 ref.execute(R, rtau)
                 ref.status()
@@ -92,14 +115,14 @@ def main():
             dist.barrier()
             torch.cuda.empty_cache()
             continue
-        mine = {j: A[j * b:(j + 1) * b].cpu().numpy() for j in own}
-        mine_tau = {k: tau[k].cpu().numpy() for k in range(kmax) if plan.owns(k)}
+        mine = {j: A[lc(j)].cpu().numpy() for j in own}
+        mine_tau = {k: tau[plan.local_index(k)].cpu().numpy() for k in own_tau}
         allcols = [None] * world
         dist.all_gather_object(allcols, (mine, mine_tau))
         say(f"run {rep}: gathered")
         if rank == 0:
             ref = tqr.TiledQR(m, n, b, dt)
-            R = A0.clone()
+            R = full_input()
             rtau = torch.zeros((kmax, m), dtype=dt, device="cuda")
             ref.execute(R, rtau)
             torch.cuda.synchronize()

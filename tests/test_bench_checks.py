@@ -109,3 +109,19 @@ def test_spawn_ranks_failure_modes(capsys):
     assert bench.spawn_ranks(2, [], popen=lambda cmd, **kw: _FakeChild(["x\n"], 0)) == 1  # no result line
     assert bench.spawn_ranks(2, [], popen=lambda cmd, **kw: _FakeChild([], 3)) == 3  # the child's code
     capsys.readouterr()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_check_owned_columns_packed_storage(world):
+    """The multi-GPU storage: a rank holds only its own tile columns, packed in column order."""
+    import tqr
+    m, n, b = 256, 128, 16
+    A0, A = _factored(m, n)
+    for rank in range(world):
+        own = tqr.owned_tile_cols(n // b, rank, world)
+        rows = torch.cat([torch.arange(j * b, (j + 1) * b) for j in own])
+        assert bench.check_owned_columns(A0[rows], A[rows], m, n, b, rank, world, own, packed=True) < 1e-12
+        Ab = A[rows].clone()
+        Ab[b + 3, 0] += 1.0  # an R entry of the rank's second tile column (row 0 <= its column)
+        with pytest.raises(RuntimeError):
+            bench.check_owned_columns(A0[rows], Ab, m, n, b, rank, world, own, packed=True)
