@@ -367,6 +367,18 @@ struct FImg {
   static constexpr int V = sizeof(S) == 8 ? FGeo<B, C>::VIMG : Img<B, S>::V;
   static constexpr int T = sizeof(S) == 8 ? FGeo<B, C>::TPIMG : Img<B, S>::T;
 };
+// The same for a counter whose adds must stay in member order: thread 0 first waits until the
+// `before` earlier members have added (no-op for the first), then adds. Rc (images of a panel
+// member out) needs it: the next member's images need only this member's factorisation (Rr), so
+// on a CU shared with another workgroup (ShapeW4) a member can finish its images before its
+// predecessor — and a chain waiting for Rc >= i-k+1 would then read member i's images unwritten.
+__device__ __forceinline__ void wg_publish_ordered(int* p, int before, int* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 && (before == 0 || spin_ge(p, before, err)))
+    __hip_atomic_fetch_add(gptr(p), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int B, typename S, class C>
 __device__ __forceinline__ size_t flow_vw_off(int p, int i, int k, int g) {
   return ((size_t)(i - k) * FGeo<B, C>::NG + g) * FImg<B, S, C>::V;
@@ -836,7 +848,8 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       }
     }
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
-    wg_publish(&a.Rc[(size_t)k * NG + g], 1);
+    // (in member order: a chain reads member i's images once Rc counts i - k + 1 members)
+    wg_publish_ordered(&a.Rc[(size_t)k * NG + g], pos, a.err);
     FST(10);
     // multi-GPU, last group (every group in ShapeW4): the images to every peer now (drained by the
     // Rt publish below, flags after it); earlier groups go during the next group's factorisation

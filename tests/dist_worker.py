@@ -75,17 +75,17 @@ def main():
             print(f"[rank {rank}] {msg}", file=sys.stderr, flush=True)
 
     # two launches back to back (stream-ordered, no host synchronisation in between), then the checks
-    As, taus = [], []
+    As, tau_list = [], []
     for rep in range(2):
         A, tau = plan.alloc_local()
         A.copy_(L0)
         As.append(A)
-        taus.append(tau)
+        tau_list.append(tau)
     for rep in range(2):
         say(f"run {rep}: execute")
-        plan.execute(As[rep], taus[rep])
+        plan.execute(As[rep], tau_list[rep])
     for rep in range(2):
-        A, tau = As[rep], taus[rep]
+        A, tau = As[rep], tau_list[rep]
         plan.status()
         say(f"run {rep}: done")
         lc = lambda j: slice(plan.local_index(j) * b, (plan.local_index(j) + 1) * b)  # noqa: E731

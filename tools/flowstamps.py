@@ -20,7 +20,12 @@ for rep in range(2):
     p.execute(A, tau)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
-nb = torch.cuda.get_device_properties(0).multi_processor_count
+gridv = ctypes.c_int()
+L.tqr_plan_info(p.h, None, None, None, ctypes.byref(gridv))
+nb = gridv.value  # workgroups of the launch (ShapeW4: two per CU)
+w4 = dt == torch.float64 and os.environ.get("TQR_FLOW_SHAPE") != "w8"
+NW = 4 if w4 else 8  # waves per workgroup
+IB = 16 if w4 else 32  # reflectors per group
 NC = 24
 st = (ctypes.c_ulonglong * (NC * nb))()
 assert L.tqr_debug_flow_stamps(st, nb) == 0
@@ -31,18 +36,18 @@ names = ["chain Rc wait in-elem other", "panel waits", "chain head-row store", "
 tot = [sum(st[w * NC + c] for w in range(nb)) for c in range(NC)]
 allt = sum(tot)
 print(f"{m}x{n} b={b}: wall {ms:.1f} ms; {nb} workgroups; sum of stamps {allt / nb / 1e5:.1f} ms per WG")
-p, q = m // b, n // b
-npanel = sum(p - k for k in range(min(p, q)))
-ng = b // 32
+pt, q = m // b, n // b
+npanel = sum(pt - k for k in range(min(pt, q)))
+ng = b // min(b, IB)
 for c, nm in ((5, "panel_factor"), (11, "build_t"), (12, "trailing"), (10, "panel I/O")):
     print(f"  per panel group ({npanel * ng} groups): {nm:14s} {tot[c] / (npanel * ng) / 100:7.2f} us")
 for c in range(NC):
     print(f"  {names[c]:24s} {tot[c] / nb / 1e5:8.2f} ms/WG  {100.0 * tot[c] / allt:5.1f}%")
 WSL = 8
-ws = (ctypes.c_ulonglong * (8 * WSL * nb))()
+ws = (ctypes.c_ulonglong * (8 * WSL * nb))()  # (g_wst holds 8 wave slots per workgroup)
 if hasattr(L, "tqr_debug_flow_wave_stamps") and L.tqr_debug_flow_wave_stamps(ws, nb) == 0:
     wn = ["drain", "barrier", "pre-sync", "post-sync", "phase1", "head I/O", "phase2", "tail"]
     print("  per-wave sums (ms/WG): " + " | ".join(f"{n:>9s}" for n in wn))
-    for w in range(8):
+    for w in range(NW):
         v = [sum(ws[b * 8 * WSL + WSL * w + c] for b in range(nb)) / nb / 1e5 for c in range(WSL)]
         print(f"    wave {w}:            " + " | ".join(f"{x:9.2f}" for x in v) + f" | sum {sum(v):7.2f}")

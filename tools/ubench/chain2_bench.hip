@@ -11,7 +11,14 @@
 // LDS-DMA'd inside it), head-row store + next head-row load, phase 2 X += V W; strip stores (sc1)
 // at the end. Data: every workgroup streams its own tile rows from HBM (ldm 16384), images from a
 // shared 64-tile pool (L2 / MALL), like the engine. TF/s counts the algorithmic TSMQR flops
-// (4 b^2 per column). MODE bits: 1 = no strip I/O, 2 = no head I/O.
+// (4 b^2 per column). MODE bits: 1 = no strip I/O, 2 = no head I/O, 4 = the engine's hand-over (the
+// finished strip stored and the next one loaded row pair by row pair inside the last group's
+// phase 2, loads trailing stores by 2 pairs), 8 = plain (write-back) strip stores instead of sc1,
+// 16 = stagger: the second half of the workgroups first runs half an element of groups without I/O
+// (two-per-CU shapes: the two workgroups of a CU out of phase, as different tasks are in the engine),
+// 32 = desync: every workgroup first runs (5 blockIdx) mod NG groups without I/O, so the element
+// hand-overs of the CUs are spread over time as in the engine (without it every CU streams its
+// strips at the same moment and the chip's HBM sees the sum as one burst).
 // Build: hipcc --offload-arch=gfx950 -O3 -I../../gpu-tiled-qr-decomposition_amd/csrc chain2_bench.hip -o chain2_bench
 #include <hip/hip_runtime.h>
 
@@ -66,6 +73,46 @@ struct Dma {
   }
 };
 
+template <int STAUX>
+struct Handover {  // the engine's XPipe: at(h) after row pair h's MFMAs, fin() after the loop
+  static constexpr int NP = B / 8, LAG = 2;
+  __amdgpu_buffer_rsrc_t out, in;
+  unsigned base;
+  __device__ __forceinline__ void st(int h, double (&X)[B / 4]) const {
+    const unsigned long long a = (unsigned long long)__double_as_longlong(X[2 * h]);
+    const unsigned long long b = (unsigned long long)__double_as_longlong(X[2 * h + 1]);
+    __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, out, base + 64 * h, 0, STAUX);
+  }
+  __device__ __forceinline__ void ld(int h, double (&X)[B / 4]) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(in, base + 64 * h, 0, 18);
+    X[2 * h] = __longlong_as_double((long long)(((unsigned long long)v[1] << 32) | v[0]));
+    X[2 * h + 1] = __longlong_as_double((long long)(((unsigned long long)v[3] << 32) | v[2]));
+  }
+  __device__ __forceinline__ void at(int h, double (&X)[B / 4]) const {
+    if (h >= 1) st(h - 1, X);
+    if (h >= 1 + LAG) ld(h - 1 - LAG, X);
+  }
+  __device__ __forceinline__ void fin(double (&X)[B / 4]) const {
+    st(NP - 1, X);
+#pragma unroll
+    for (int h = NP - 1 - LAG; h < NP; ++h) ld(h, X);
+  }
+};
+template <int STAUX>
+__device__ __forceinline__ void store_strip_aux(const double (&X)[B / 4], double* tile) {
+  const int lane = threadIdx.x & 63, x = lane >> 4, c = lane & 15;
+  const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile);
+  const unsigned base = (unsigned)(((size_t)c * LDM + 2 * x) * sizeof(double));
+#pragma unroll
+  for (int h = 0; h < B / 8; ++h) {
+    const unsigned long long a = (unsigned long long)__double_as_longlong(X[2 * h]);
+    const unsigned long long b = (unsigned long long)__double_as_longlong(X[2 * h + 1]);
+    __attribute__((ext_vector_type(4))) unsigned v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, base, 64 * h, STAUX);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void sync_cnt() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
@@ -92,18 +139,36 @@ __global__ __launch_bounds__(64 * NW, WPC) void k_chain(double* X0, double* H0, 
     Dma<NW, IB> d{lds, vimg(0, 0), vimg(0, 0) + Im<IB>::V};
     for (int m = 0; m < Dma<NW, IB>::STEPS; ++m) d.step(m);
   }
-  if (MODE & 1) load_strip_pair<B, double>(X, Xs, LDM, 0);
+  constexpr int STAUX = (MODE & 8) ? 0 : 16;
+  constexpr bool XP = (MODE & 4) && !(MODE & 1);
+  if ((MODE & 1) || (MODE & 48)) load_strip_pair<B, double>(X, Xs, LDM, 0);
+  const int pre = (MODE & 32) ? (5 * blockIdx.x) % NG : (MODE & 16) && blockIdx.x >= gridDim.x / 2 ? NG / 2 : 0;
+  if (pre > 0) {  // stagger / desync: groups without I/O first
+    for (int g = 0; g < pre; ++g) {
+      sync_cnt<0>();
+      const double* Vs = lds + buf * BUF;
+      Dma<NW, IB> d{lds + (buf ^ 1) * BUF, vimg(0, (g + 1) % NG), vimg(0, (g + 1) % NG) + Im<IB>::V};
+      apply_zw<B, true, Dma<NW, IB>, true, true, true, IB>(Vs, Vs + Im<IB>::V, X, H, W, 0, d);
+      apply_x4<B, NoPost, IB>(Vs, X, W);
+      buf ^= 1;
+    }
+    sync_cnt<0>();
+    Dma<NW, IB> d{lds + buf * BUF, vimg(0, 0), vimg(0, 0) + Im<IB>::V};
+    for (int m = 0; m < Dma<NW, IB>::STEPS; ++m) d.step(m);
+  }
+  bool xin = false;
   for (int e = 0; e < nelem; ++e) {
     const int ti = e % NTILE;
     double* Xt = Xs + (size_t)ti * B;
     if (!(MODE & 2)) load_head_pair<B, 16, IB>(H, hrs, hoff);
-    if (!(MODE & 1)) load_strip_pair<B, double>(X, Xt, LDM, 0);
+    if (!(MODE & 1) && !xin) load_strip_pair<B, double>(X, Xt, LDM, 0);
     for (int g = 0; g < NG; ++g) {
       // the group's DMA (issued in the previous group's phase 1) and everything older complete; the
       // youngest operations (this element's strip / head loads, the previous group's head stores and
       // this group's head loads) may still be in flight
       constexpr int NX = ((MODE & 1) ? 0 : NKS / 2) + ((MODE & 2) ? 0 : NRI / 2), NH = (MODE & 2) ? 0 : NRI;
       if (g == 0) sync_cnt<NX>();
+      else if (XP && xin && g == 1) sync_cnt<0>();  // (the streamed hand-over's stores drained)
       else sync_cnt<NH>();
       const double* Vs = lds + buf * BUF;
       const double* Ts = Vs + Im<IB>::V;
@@ -114,10 +179,17 @@ __global__ __launch_bounds__(64 * NW, WPC) void k_chain(double* X0, double* H0, 
         store_head_pair<B, 0, IB>(H, hrs, hoff + g * IB * 8);
         if (g + 1 < NG) load_head_pair<B, 18, IB>(H, hrs, hoff + (g + 1) * IB * 8);
       }
-      apply_x4<B, NoPost, IB>(Vs, X, W);
+      if (XP && g + 1 == NG && e + 1 < nelem) {
+        const Handover<STAUX> hp{uniform_rsrc(Xt), uniform_rsrc(Xs + (size_t)((e + 1) % NTILE) * B),
+                                 (unsigned)((((size_t)(t & 15)) * LDM + 2 * ((t & 63) >> 4)) * sizeof(double))};
+        apply_x4<B, Handover<STAUX>, IB>(Vs, X, W, hp);
+      } else {
+        apply_x4<B, NoPost, IB>(Vs, X, W);
+      }
       buf ^= 1;
     }
-    if (!(MODE & 1)) store_strip_pair<B, double>(X, Xt, LDM, 0);
+    xin = XP && e + 1 < nelem;
+    if (!(MODE & 1) && !xin) store_strip_aux<STAUX>(X, Xt);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -184,11 +256,14 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   printf("%d CUs, %d elements per workgroup (tile rows streamed from HBM, ldm %ld)\n", ncu, nelem, LDM);
   if (run<8, 32, 0, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
+  if (run<8, 32, 32, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
+  if (run<8, 32, 40, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
+  if (run<8, 32, 33, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
+  if (run<8, 32, 35, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
   if (run<4, 16, 0, 2>("w4ib16", X, H, img, ncu, nelem, clk)) return 1;
-  if (run<4, 32, 0, 1>("w4ib32", X, H, img, ncu, nelem, clk)) return 1;
-  if (run<8, 32, 1, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
-  if (run<4, 16, 1, 2>("w4ib16", X, H, img, ncu, nelem, clk)) return 1;
-  if (run<8, 32, 3, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
-  if (run<4, 16, 3, 2>("w4ib16", X, H, img, ncu, nelem, clk)) return 1;
+  if (run<4, 16, 32, 2>("w4ib16", X, H, img, ncu, nelem, clk)) return 1;
+  if (run<4, 16, 40, 2>("w4ib16", X, H, img, ncu, nelem, clk)) return 1;
+  if (run<4, 16, 33, 2>("w4ib16", X, H, img, ncu, nelem, clk)) return 1;
+  if (run<4, 16, 35, 2>("w4ib16", X, H, img, ncu, nelem, clk)) return 1;
   return 0;
 }
