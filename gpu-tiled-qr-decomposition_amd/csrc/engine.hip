@@ -317,9 +317,9 @@ static void get_kernels(kfn* p, kfn* u, kfn* t) {
   *t = k_build_t<B, S>;
 }
 typedef void (*ffn)(FlowArgs);
-// Engine shape of the persistent kernel (flow.hpp FlowShape): 4 = ShapeW4 (two 4-wave workgroups
-// per CU, 64-column strips, 16-reflector groups; the fp64 default), 8 = ShapeW8 (one 8-wave
-// workgroup per CU, 128-column strips, 32-reflector groups; fp32, and fp64 with TQR_FLOW_SHAPE=w8)
+// Engine shape of the persistent kernel (flow.hpp FlowShape): 8 = ShapeW8 (one 8-wave workgroup per
+// CU, 128-column strips, 32-reflector groups; the default), 4 = ShapeW4 (two 4-wave workgroups per
+// CU, 64-column strips, 16-reflector groups; fp64 with TQR_FLOW_SHAPE=w4)
 struct ShapeInfo {
   int nw, nt, sw, ib, wpc;
 };
@@ -327,10 +327,12 @@ static ShapeInfo shape_info(int shape) {
   return shape == 4 ? ShapeInfo{ShapeW4::NW, ShapeW4::NT, ShapeW4::SW, ShapeW4::IB, ShapeW4::WPC}
                     : ShapeInfo{ShapeW8::NW, ShapeW8::NT, ShapeW8::SW, ShapeW8::IB, ShapeW8::WPC};
 }
+// fp64 default: ShapeW8 — ShapeW4 measured 138.6-139.0 vs 126.7-126.9 ms at 16384^2 (two alternating
+// A/B rounds on one box, profiles/r04/shape_ab); TQR_FLOW_SHAPE=w4 selects it
 static int flow_shape(int dtype) {
   if (dtype != TQR_F64) return 8;
   const char* e = getenv("TQR_FLOW_SHAPE");
-  return e && strcmp(e, "w8") == 0 ? 8 : 4;
+  return e && strcmp(e, "w4") == 0 ? 4 : 8;
 }
 static int shape_ib(int shape, int b) { return std::min(b, shape_info(shape).ib); }
 static int shape_ns(int shape, int b) { const int sw = shape_info(shape).sw; return (b + sw - 1) / sw; }

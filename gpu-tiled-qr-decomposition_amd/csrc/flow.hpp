@@ -122,12 +122,13 @@ constexpr int FLOW_SW = 16 * FLOW_NW;      // strip width (columns) of a chain t
 constexpr bool FLOW_PF = true;
 
 // Engine shapes. ShapeW8 is the form above (one 8-wave workgroup per CU, 128-column chain strips,
-// 32-reflector groups): the fp32 engine, and fp64 under TQR_FLOW_SHAPE=w8. ShapeW4 (round 4, the
-// fp64 default): TWO independent 4-wave workgroups per CU, 64-column chain strips, 16-reflector
-// groups — half the LDS images (76 KiB per workgroup, so two fit in the CU's 160 KiB), and the two
-// workgroups run different tasks: one's strip hand-over (its stores' acknowledgement on the shared
-// vmcnt), barrier skew and dependent-MFMA tails run beside the other's MFMA stream instead of
-// idling the CU's matrix pipes (tools/ubench/chain2_bench.hip).
+// 32-reflector groups): the default. ShapeW4 (round 4, fp64 under TQR_FLOW_SHAPE=w4): TWO
+// independent 4-wave workgroups per CU, 64-column chain strips, 16-reflector groups — half the LDS
+// images (76 KiB per workgroup, so two fit in the CU's 160 KiB), the two workgroups running
+// different tasks, so that one's strip hand-over, barrier skew and dependent-MFMA tails could run
+// beside the other's MFMA stream. Measured: no gain — the chain loop alone is 3-4 % slower
+// (tools/ubench/chain2_bench.hip: the hand-over's cost is not hidden by the co-resident workgroup,
+// with or without the two out of phase) and the factorisation 9 % (138.6 vs 126.7 ms at 16384^2).
 template <int NW_, int IB_, int WPC_>
 struct FlowShape {
   static constexpr int NW = NW_, NT = 64 * NW_, SW = 16 * NW_, IB = IB_, WPC = WPC_;
