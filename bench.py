@@ -344,6 +344,11 @@ def main():
     dt = torch.float64 if args.storage == "f64" else torch.float32
     q = n // b
     rehearsal = world > 1 and "TQR_BENCH_DEVICE" in os.environ
+    if rehearsal and "TQR_FLOW_GRID" not in os.environ:
+        # ranks sharing one GPU: each persistent launch gets its share of the CUs (all ranks' launches
+        # must be resident together — a rank's chains wait for its peers' panels inside the launch)
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        os.environ["TQR_FLOW_GRID"] = str(max(1, ncu // world))
 
     # strong scaling, self-contained: before the N-rank region, rank 0 factorises the same m x n
     # matrix on its GPU alone (single-GPU engine, same steps / warmup / input handling); the others wait
@@ -565,8 +570,9 @@ def main():
             "data": "synthetic (RANDZO distribution, device-generated)",
             "config": {"workload": f"tiled QR {m}x{n} {args.storage} storage, tile {b} (BASELINE configs[{cfg}])", "m": m, "n": n,
                        "tile": b, "parallelism": "single GPU" if world == 1 else
-                       (f"{world} ranks on ONE GPU (rehearsal, TQR_BENCH_DEVICE), tile-column {part}, panel V/T "
-                        "forwarded device to device" if rehearsal else
+                       (f"{world} ranks on ONE GPU (rehearsal, TQR_BENCH_DEVICE; {os.environ.get('TQR_FLOW_GRID')} "
+                        f"workgroups per rank, the single-GPU leg too), tile-column {part}, panel V/T forwarded device to "
+                        "device" if rehearsal else
                         f"{world} GPUs, tile-column {part}, panel V/T forwarded over xGMI"),
                        "inputs": "one resident copy per timed step, staged before the timed region" if staged
                        else "input restored by a device copy inside each timed step"},

@@ -23,7 +23,7 @@ for rep in range(2):
 gridv = ctypes.c_int()
 L.tqr_plan_info(p.h, None, None, None, ctypes.byref(gridv))
 nb = gridv.value  # workgroups of the launch (ShapeW4: two per CU)
-w4 = dt == torch.float64 and os.environ.get("TQR_FLOW_SHAPE") != "w8"
+w4 = dt == torch.float64 and os.environ.get("TQR_FLOW_SHAPE") == "w4"
 NW = 4 if w4 else 8  # waves per workgroup
 IB = 16 if w4 else 32  # reflectors per group
 NC = 24
