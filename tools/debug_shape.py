@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(REPO, "gpu-tiled-qr-decomposition_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 import tqr  # noqa: E402
 
-b = 256
+b = int(os.environ.get("TQR_DBG_B", "256"))
 sizes = [int(x) for x in sys.argv[1:]] or [2048, 4096, 8192, 16384]
 for n in sizes:
     m = n
