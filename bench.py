@@ -229,6 +229,13 @@ def single_gpu_leg(tqr, torch, m, n, b, dt, steps, warmup):
             "t1_column_norm_rel_err": rel}
 
 
+def seglen_of(world, full=True):
+    """The engine's chain segment length for a plan of `world` ranks (engine.hip env_seglen); full:
+    each rank's launch covers its whole device (not a one-GPU rehearsal's share)."""
+    e = os.environ.get("TQR_SEGLEN")
+    return max(1, int(e)) if e else (2 if world >= 4 and full else 8)
+
+
 def launch_plan(gpus, env, ndev):
     """How `bench.py --gpus N` runs: ("run", None) in this process (N = 1, or already one rank of an
     external torch.distributed.run), ("spawn", None) = start N ranks as a child launcher, or
@@ -344,11 +351,12 @@ def main():
     dt = torch.float64 if args.storage == "f64" else torch.float32
     q = n // b
     rehearsal = world > 1 and "TQR_BENCH_DEVICE" in os.environ
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     if rehearsal and "TQR_FLOW_GRID" not in os.environ:
         # ranks sharing one GPU: each persistent launch gets its share of the CUs (all ranks' launches
         # must be resident together — a rank's chains wait for its peers' panels inside the launch)
-        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
         os.environ["TQR_FLOW_GRID"] = str(max(1, ncu // world))
+    full_grid = int(os.environ.get("TQR_FLOW_GRID", ncu)) >= ncu  # (engine.hip: the segment-length rule)
 
     # strong scaling, self-contained: before the N-rank region, rank 0 factorises the same m x n
     # matrix on its GPU alone (single-GPU engine, same steps / warmup / input handling); the others wait
@@ -575,7 +583,9 @@ def main():
                         "device" if rehearsal else
                         f"{world} GPUs, tile-column {part}, panel V/T forwarded over xGMI"),
                        "inputs": "one resident copy per timed step, staged before the timed region" if staged
-                       else "input restored by a device copy inside each timed step"},
+                       else "input restored by a device copy inside each timed step",
+                       # elements per chain task (engine.hip env_seglen: TQR_SEGLEN, else 2 at >= 4 ranks, 8 otherwise)
+                       "chain_segment_length": seglen_of(world, full_grid)},
             "roofline": roof,
             "cpu_baseline": cpu,
             "check": {"column_norm_rel_err": ok_rel} if ok_rel is not None else None,

@@ -493,9 +493,18 @@ static FlowKnobs knobs_from_env(int seglen) {
   if (const char* elac = getenv("TQR_LAC")) kn.lac = atof(elac);  // lookahead column's chains (default: TQR_LA)
   return kn;
 }
-static int env_seglen() {
+// Chain segment length (elements per chain task; TQR_SEGLEN overrides). 8, except for 4 and more
+// ranks with a whole device each (1024+ workgroups in all): 2 — more, shorter chain tasks give
+// each rank work it can start while its columns' wavefronts (the head rows going down a column)
+// wait on other ranks' panels. The model of the 8-GPU run (tools/sched_sim_seglen.py, per-segment
+// cost calibrated on one MI355X) gives S(8) 6.17 at length 2 against 5.44 at 8; one GPU pays
+// 4.6 % for length 2 (65536x16384: 635.3 vs 607.6 ms), and so do the one-GPU rehearsals (4 ranks
+// x 64 CUs: 645.8 vs 628.8 ms; model 600.5 vs 575.1), whose ranks have work to spare.
+// full: the rank's launch covers its whole device (every rank must decide alike — tqr_dist_import
+// checks the ranks' task-list signatures).
+static int env_seglen(int world = 1, bool full = true) {
   const char* sl = getenv("TQR_SEGLEN");
-  return sl ? std::max(1, atoi(sl)) : 8;
+  return sl ? std::max(1, atoi(sl)) : (world >= 4 && full ? 2 : 8);
 }
 
 // ns: chain strips per tile column, ng: reflector groups per tile (the engine shape's, shape_ns /
@@ -735,6 +744,7 @@ struct tqr_plan {
   int engine = 1;          // 1 = persistent dataflow (default), 0 = wave-batched launches
   Item* d_flow = nullptr;
   int nflow = 0;
+  int nflow_global = 0;  // tasks of the global list (before a multi-GPU partition)
   int* d_sync = nullptr;   // next, err, Rc, Tc, Ac, Rt, Rr
   size_t sync_ints = 0;
   int ns = 1, ng = 1, grid = 256, est_order = 0;
@@ -954,9 +964,18 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
   pl->ns = shape_ns(pl->shape, b);  // chain strips per tile
   pl->ng = b / shape_ib(pl->shape, b);  // reflector groups per tile
   if (pl->engine == TQR_ENGINE_FLOW) {
+    int dev = 0;
+    hipDeviceProp_t pr;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&pr, dev) != hipSuccess) {
+      tqr_plan_destroy(pl); return TQR_EHIP;
+    }
+    const int full_grid = pr.multiProcessorCount * shape_info(pl->shape).wpc;  // (ShapeW4: two workgroups per CU)
+    pl->grid = full_grid;
+    if (const char* gs = getenv("TQR_FLOW_GRID")) pl->grid = std::max(1, atoi(gs));
     FlowPlan fp;
-    pl->knobs = knobs_from_env(env_seglen());
+    pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid));
     build_flow_plan(pl->p, pl->q, pl->ns, pl->ng, pl->knobs, fp);
+    pl->nflow_global = (int)fp.items.size();
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
@@ -1001,14 +1020,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     }
     pl->kflow = resolve_flow(b, dtype, pl->shape);
     pl->ldsF = lds_flow(b, dtype, pl->shape);
-    int dev = 0;
-    hipDeviceProp_t pr;
-    if (!pl->kflow || hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&pr, dev) != hipSuccess) {
-      tqr_plan_destroy(pl); return TQR_EHIP;
-    }
-    pl->grid = pr.multiProcessorCount * shape_info(pl->shape).wpc;  // (ShapeW4: two workgroups per CU)
-    const char* gs = getenv("TQR_FLOW_GRID");
-    if (gs) pl->grid = std::max(1, atoi(gs));
+    if (!pl->kflow) { tqr_plan_destroy(pl); return TQR_EHIP; }
   }
   *out = pl;
   return TQR_OK;
@@ -1031,8 +1043,14 @@ int tqr_plan_status(tqr_plan* pl, void* stream) {
 // handle block: the PCI bus id of the exporting device (64 bytes), then the IPC handles of its
 // member flags and of its per-step panel workspaces
 static constexpr size_t kBusIdBytes = 64;
+// a rank's handle: PCI bus id, the task-list signature (every rank must partition the same global
+// list: segment lengths, lookahead tail, list length), the IPC handles of Rf and the workspaces
+constexpr size_t kSigInts = 4;
+static void plan_signature(const tqr_plan* pl, int* sig) {
+  sig[0] = pl->knobs.seglen; sig[1] = pl->knobs.seglen_la; sig[2] = pl->knobs.la_tail; sig[3] = pl->nflow_global;
+}
 size_t tqr_dist_handle_bytes(const tqr_plan* pl) {
-  return pl ? kBusIdBytes + sizeof(hipIpcMemHandle_t) * (1 + (size_t)pl->kmax) : 0;
+  return pl ? kBusIdBytes + sizeof(int) * kSigInts + sizeof(hipIpcMemHandle_t) * (1 + (size_t)pl->kmax) : 0;
 }
 
 int tqr_dist_export(tqr_plan* pl, void* buf, size_t len) {
@@ -1044,8 +1062,11 @@ int tqr_dist_export(tqr_plan* pl, void* buf, size_t len) {
   std::vector<hipIpcMemHandle_t> h(1 + pl->kmax);
   HIPCHK(hipIpcGetMemHandle(&h[0], pl->d_rf));
   for (int k = 0; k < pl->kmax; ++k) HIPCHK(hipIpcGetMemHandle(&h[1 + k], pl->wk[k]));
+  int sig[kSigInts];
+  plan_signature(pl, sig);
   memcpy(buf, bus, kBusIdBytes);
-  memcpy((char*)buf + kBusIdBytes, h.data(), sizeof(hipIpcMemHandle_t) * h.size());
+  memcpy((char*)buf + kBusIdBytes, sig, sizeof(sig));
+  memcpy((char*)buf + kBusIdBytes + sizeof(sig), h.data(), sizeof(hipIpcMemHandle_t) * h.size());
   return TQR_OK;
 }
 
@@ -1098,13 +1119,23 @@ int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
       continue;
     }
     const char* blk = (const char*)all + (size_t)r * hb;
+    int sig[kSigInts], mine[kSigInts];
+    memcpy(sig, blk + kBusIdBytes, sizeof(sig));
+    plan_signature(pl, mine);
+    if (memcmp(sig, mine, sizeof(sig)) != 0) {  // a launch over different lists would deadlock
+      fprintf(stderr, "tqr: rank %d and rank %d built different task lists (segment lengths %d/%d vs %d/%d, "
+              "lookahead tail %d vs %d, %d vs %d tasks): set TQR_SEGLEN / TQR_FLOW_GRID alike on every rank\n",
+              pl->rank, r, mine[0], mine[1], sig[0], sig[1], mine[2], sig[2], mine[3], sig[3]);
+      close_opened(pl);
+      return TQR_EINVAL;
+    }
     char bus[kBusIdBytes];
     memcpy(bus, blk, kBusIdBytes);
     bus[kBusIdBytes - 1] = 0;
     int st = enable_peer(pl->rank, r, bus);
     if (st) { close_opened(pl); return st; }
     std::vector<hipIpcMemHandle_t> h(1 + pl->kmax);
-    memcpy(h.data(), blk + kBusIdBytes, hb - kBusIdBytes);
+    memcpy(h.data(), blk + kBusIdBytes + sizeof(sig), hb - kBusIdBytes - sizeof(sig));
     for (int x = 0; x <= pl->kmax; ++x) {
       void* p = nullptr;
       if (hipIpcOpenMemHandle(&p, h[x], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {

@@ -121,11 +121,16 @@ long tqr_total_tasks(int m, int n, int b);
  * number of times; consecutive executes need no host synchronisation or barrier between the
  * ranks (the cross-rank flags carry launch epochs, and a rank forwards into a peer only once that
  * peer's previous launch has finished, all on the device).
+ * Chain tasks are shorter on 4+ ranks that each launch over a whole device (2 elements instead of
+ * 8; TQR_SEGLEN overrides): more parallel slack per rank. Every rank must build the
+ * same global task list — tqr_dist_import compares the ranks' list signatures (segment lengths,
+ * lookahead tail, list length) and fails with TQR_EINVAL if they differ.
  * Setup once: tqr_dist_export -> exchange all ranks' handle blocks (e.g. an all-gather over
  * torch.distributed / MPI) -> tqr_dist_import(plan, blocks of rank 0..world-1). */
 int tqr_dist_plan_create(tqr_plan** plan, int m, int n, int b, int dtype, int rank, int world);
-/* bytes of one rank's handle block (IPC handles of its panel counters and per-step panel
- * workspaces — one allocation per step keeps every export under 2 GiB) */
+/* bytes of one rank's handle block (its device's PCI bus id, its task-list signature, the IPC
+ * handles of its panel counters and per-step panel workspaces — one allocation per step keeps
+ * every export under 2 GiB) */
 size_t tqr_dist_handle_bytes(const tqr_plan* plan);
 int tqr_dist_export(tqr_plan* plan, void* handles, size_t len);
 int tqr_dist_import(tqr_plan* plan, const void* all_handles, size_t len);

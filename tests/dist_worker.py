@@ -46,7 +46,13 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     q, kmax = n // b, min(m, n) // b
+    # test hooks: rank 1 builds its task list with another segment length (must fail at import);
+    # the single-GPU reference with its own segment length (results are bit-identical regardless)
+    if rank == 1 and os.environ.get("TQR_TEST_SEGLEN_RANK1"):
+        os.environ["TQR_SEGLEN"] = os.environ["TQR_TEST_SEGLEN_RANK1"]
     plan = tqr.DistTiledQR(m, n, b, dt)
+    if os.environ.get("TQR_TEST_REF_SEGLEN"):
+        os.environ["TQR_SEGLEN"] = os.environ["TQR_TEST_REF_SEGLEN"]
     L0, _ = plan.alloc_local()
     plan.fill_randzo_local(L0, 5)
     own = plan.owned_cols()

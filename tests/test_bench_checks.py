@@ -125,3 +125,13 @@ def test_check_owned_columns_packed_storage(world):
         Ab[b + 3, 0] += 1.0  # an R entry of the rank's second tile column (row 0 <= its column)
         with pytest.raises(RuntimeError):
             bench.check_owned_columns(A0[rows], Ab, m, n, b, rank, world, own, packed=True)
+
+
+def test_chain_segment_length_rule(monkeypatch):
+    """bench.seglen_of mirrors engine.hip env_seglen: 8 on one or two ranks, 2 from four ranks on
+    (tools/sched_sim_seglen.py), TQR_SEGLEN overrides."""
+    monkeypatch.delenv("TQR_SEGLEN", raising=False)
+    assert [bench.seglen_of(w) for w in (1, 2, 4, 8)] == [8, 8, 2, 2]
+    assert bench.seglen_of(4, full=False) == 8  # one-GPU rehearsal: a share of the CUs per rank
+    monkeypatch.setenv("TQR_SEGLEN", "5")
+    assert bench.seglen_of(8) == 5 and bench.seglen_of(1) == 5

@@ -100,13 +100,15 @@ def test_partition_gloo_world2():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("m,n,b,dt,ranks,mode", [(1024, 1024, 128, "f64", 2, "gather"), (2048, 768, 256, "f64", 2, "gather"),
-                                                 (512, 1024, 64, "f64", 2, "gather"), (1024, 512, 128, "f32", 2, "gather"),
-                                                 (2048, 2048, 256, "f64", 4, "gather"),
-                                                 # BASELINE configs[3] shape at full size
-                                                 (65536, 16384, 256, "f64", 2, "checksum")])
-def test_ranks_on_one_gpu_match_single_gpu(m, n, b, dt, ranks, mode):
-    env = dict(os.environ, TQR_FLOW_GRID=str(192 // ranks))
+@pytest.mark.parametrize("m,n,b,dt,ranks,mode,extra", [(1024, 1024, 128, "f64", 2, "gather", {}), (2048, 768, 256, "f64", 2, "gather", {}),
+                                                       (512, 1024, 64, "f64", 2, "gather", {}), (1024, 512, 128, "f32", 2, "gather", {}),
+                                                       (2048, 2048, 256, "f64", 4, "gather", {}),
+                                                       # the 8-GPU default segment length (2) against one GPU's (8)
+                                                       (2048, 2048, 256, "f64", 4, "gather", {"TQR_SEGLEN": "2", "TQR_TEST_REF_SEGLEN": "8"}),
+                                                       # BASELINE configs[3] shape at full size
+                                                       (65536, 16384, 256, "f64", 2, "checksum", {})])
+def test_ranks_on_one_gpu_match_single_gpu(m, n, b, dt, ranks, mode, extra):
+    env = dict(os.environ, TQR_FLOW_GRID=str(192 // ranks), **extra)
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr=127.0.0.1", f"--master-port={port}",
@@ -119,3 +121,19 @@ def test_ranks_on_one_gpu_match_single_gpu(m, n, b, dt, ranks, mode):
         assert res[run]["cols_covered"]
         # same tile operations in the same order on every rank: bit-identical to one GPU
         assert res[run]["exact"], res[run]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_ranks_with_different_task_lists_fail_at_import():
+    """A rank whose task list differs (here its chain segment length) would deadlock the launch:
+    tqr_dist_import compares the ranks' list signatures and both ranks fail cleanly instead."""
+    env = dict(os.environ, TQR_FLOW_GRID="96", TQR_TEST_SEGLEN_RANK1="4")
+    env.pop("TQR_SEGLEN", None)
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.join(HERE, "dist_worker.py"), "1024", "1024", "128", "f64", "0", "gather"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0
+    assert "built different task lists" in r.stderr, r.stderr[-2000:]

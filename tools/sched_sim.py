@@ -277,7 +277,7 @@ def owner_of(j, world, kind="cyclic"):
 
 
 def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="idle", trace=None, pres=0,
-                  part="snake"):
+                  part="snake", fine=None):
     """The engine on `world` GPUs of W workgroups each: rank r runs the tasks of the global list
     that it owns (chains of tile column j and panel j on owner_of(j)) in list order. A
     chain whose panel lives on another rank waits for the member flags instead of Rc: the owner
@@ -287,10 +287,16 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
     path), flags after its Rt publish; mode "idle" (round 3): waves 4-7 copy group g's images during
     the factorisation of group g+1 (stretching it only if the copy is longer), flags at its end;
     the last group inline. pres > 0: each rank reserves `pres` of its W workgroups for panel tasks
-    (a second in-order queue), the others take chain tasks only. Returns the makespan (us)."""
+    (a second in-order queue), the others take chain tasks only.
+    fine = (df, dt): column-granular member hand-off (a what-if, not the engine): member i+1's
+    reflector step C waits for member i's step C (not its whole group): its factorisation of group
+    g starts df us after member i's started and ends no earlier than df after member i's ended;
+    its trailing update likewise trails member i's by dt (strip-granular). Returns the makespan (us)."""
     NG, W = prm["NG"], prm["W"]
     fw = fwd_peer * (world - 1)
     Rr, Rc, E, FL, Tc, G = {}, {}, {}, {}, {}, {}
+    FS, TcR, GR = {}, {}, {}
+    x2d = hop + 3.0  # "2d": a strip / head-row hand-over between ranks (flag hop + 256 KiB over xGMI)
     heaps = [[0.0] * (W - pres) for _ in range(world)]
     pheaps = [[0.0] * pres for _ in range(world)]
     span = 0.0
@@ -301,28 +307,37 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
             r = owner_of(k, world, part)
         else:
             k, j = kk & 0xffff, m
-            r = owner_of(j, world, part)
+            r = owner_of(j, world, "snake" if part == "2d" else part)
+            if part == "2d":  # what-if: chain segments spread over the ranks, not by column
+                r = (j + (kk >> 16)) % world
         hp = pheaps[r] if (pres and typ != 4) else heaps[r]
         t0 = heapq.heappop(hp) + prm["disp"]
         if typ != 4:
             t = t0
             if k > 0:
-                t = max([t] + [Tc[(i, k, s, k - 1)] for s in range(ns)])
+                t = max([t] + [Tc[(i, k, s, k - 1)] + (x2d if TcR[(i, k, s, k - 1)] != r else 0.0) for s in range(ns)])
             rr, rc, ee, fl = [0.0] * NG, [0.0] * NG, [0.0] * NG, [0.0] * NG
+            fs = [0.0] * NG
             prev = (i - 1, k) if i > k else None
             for g in range(NG):
                 gs = t if g == 0 else ee[g - 1]
                 if prev:
-                    gs = max(gs, Rr[prev][g])
+                    gs = max(gs, FS[prev][g] + fine[0]) if fine else max(gs, Rr[prev][g])
+                fs[g] = gs
                 fct = prm["f"]
                 if world > 1 and mode == "idle" and g > 0:
                     fct = max(fct, fw)  # waves 4-7 copy group g-1 meanwhile
                 rr[g] = gs + prm["io_in"] + fct + prm["io_wb"]
+                if prev and fine:
+                    rr[g] = max(rr[g], Rr[prev][g] + fine[0])
                 rc[g] = rr[g] + prm["bt"] + prm["io_img"]
                 last = g + 1 == NG
                 inline = world > 1 and (mode == "inline" or last)
                 ready = rc[g] + (fw if inline else 0.0)
-                ee[g] = (max(ready, E[prev][g]) if prev else ready) + prm["t"]
+                if prev and fine:
+                    ee[g] = max(ready + prm["t"], E[prev][g] + fine[1])
+                else:
+                    ee[g] = (max(ready, E[prev][g]) if prev else ready) + prm["t"]
                 if world > 1:
                     if inline:
                         fl[g] = ee[g] + hop
@@ -331,6 +346,7 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
                 if world > 1 and mode == "idle" and g > 0:
                     fl[g - 1] = rr[g] - prm["io_wb"] + hop
             Rr[(i, k)], Rc[(i, k)], E[(i, k)], FL[(i, k)] = rr, rc, ee, fl
+            FS[(i, k)] = fs
             end = ee[-1]
         else:
             s = (ts >> 8) & 0xff
@@ -338,12 +354,14 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
             e = kk >> 16
             remote = world > 1 and owner_of(k, world, part) != r
             rows = ([k] if e == 0 else []) + list(range(i0, i1))
-            t = t0
+            t = t0 + prm.get("seg", 0.0)  # per-segment cost (head rows in / out, Ac hand-over)
             pg = G[(k, j, s, e - 1)] if e > 0 else None
+            if pg is not None and GR[(k, j, s, e - 1)] != r:
+                pg = [x + x2d for x in pg]
             lastg = None
             for idx, i in enumerate(rows):
                 if k > 0:
-                    t = max(t, Tc[(i, j, s, k - 1)])
+                    t = max(t, Tc[(i, j, s, k - 1)] + (x2d if TcR[(i, j, s, k - 1)] != r else 0.0))
                 t += prm["e_ld"]
                 av = FL[(i, k)] if remote else Rc[(i, k)]
                 nxt = (FL if remote else Rc)[(rows[idx + 1], k)][0] if idx + 1 < len(rows) else 0.0
@@ -357,13 +375,190 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
                     g_t[g] = t
                 t += prm["e_st"]
                 Tc[(i, j, s, k)] = t
+                TcR[(i, j, s, k)] = r
                 lastg = g_t
             G[(k, j, s, e)] = lastg
+            GR[(k, j, s, e)] = r
             end = t
         span = max(span, end)
         heapq.heappush(hp, end)
         if trace is not None:
             trace.append((r, t0, end, typ, k))
+    return span
+
+
+def simulate_dist_dyn(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, part="snake", prio="list",
+                      waits=None):
+    """Dependency-triggered dispatch (the reference's completeATask -> cuda_queue_puttask,
+    gpucalc.cu:691-814 / 195-225, per rank): each rank keeps a ready queue fed by completions —
+    its local counters and the peers' member flags — and a free workgroup takes the best task whose
+    first useful work can start now (its dependencies' times are known and reached), else waits
+    for the earliest one. Nothing is dequeued that would hold a workgroup waiting for its start;
+    waits inside a task (later groups / elements) remain. prio "list": the engine's list position;
+    "class": panels, then the lookahead column's chains, then other chains, each by (step, column).
+    Timing rules as simulate_dist (idle-wave forwarding). Returns the makespan (us)."""
+    NG, W = prm["NG"], prm["W"]
+    fw = fwd_peer * (world - 1)
+    wt = waits if waits is not None else {}
+    acc = lambda c, v: wt.__setitem__(c, wt.get(c, 0.0) + max(0.0, v))
+    tasks = []
+    for x, (ts, l, m, kk) in enumerate(items):
+        typ = ts & 0xff
+        if typ != 4:
+            tasks.append(("P", l, kk, x))
+        else:
+            s = (ts >> 8) & 0xff
+            tasks.append(("C", kk & 0xffff, m, s, kk >> 16, l & 0xffff, l >> 16, x))
+    rank_of = lambda t: owner_of(t[2], world, part) if t[0] == "P" else owner_of(t[2], world, part)
+    segl = {}
+    for t in tasks:  # segment index of row i in chain (k, j): from the list's own segments
+        if t[0] == "C":
+            _, k, j, s, e, i0, i1, _ = t
+            for i in range(i0, i1):
+                segl[(k, j, i)] = e
+    deps = {}
+    for t in tasks:
+        if t[0] == "P":
+            _, i, k, _ = t
+            d = [("P", i - 1, k)] if i > k else []
+            if k > 0:
+                d += [("C", k - 1, k, s, segl[(k - 1, k, i)]) for s in range(ns)]
+        else:
+            _, k, j, s, e, i0, i1, _ = t
+            d = [("P", k, k)] if e == 0 else [("C", k, j, s, e - 1)]
+            for i in ([k] if e == 0 else []) + list(range(i0, i1)):
+                if i > k:
+                    d.append(("P", i, k))
+                if k > 0:
+                    d.append(("C", k - 1, j, s, segl[(k - 1, j, i)]))
+        deps[t] = set(d)
+    key = lambda t: t[:3] if t[0] == "P" else t[:5]
+    succ, ndep = {}, {}
+    for t in tasks:
+        ndep[key(t)] = len(deps[t])
+        for d in deps[t]:
+            succ.setdefault(d, []).append(t)
+    Rr, Rc, E, FL, Tc, G = {}, {}, {}, {}, {}, {}
+
+    def ready_time(t):
+        if t[0] == "P":
+            _, i, k, _ = t
+            r = max([Tc[(i, k, s, k - 1)] for s in range(ns)]) if k > 0 else 0.0
+            if i > k:
+                r = max(r, Rr[(i - 1, k)][0])
+            return r
+        _, k, j, s, e, i0, i1, _ = t
+        i = k if e == 0 else i0
+        remote = world > 1 and owner_of(k, world, part) != owner_of(j, world, part)
+        av = (FL if remote else Rc)[(i, k)]
+        r = max(av[0], av[1] if NG > 1 else av[0])
+        if k > 0:
+            r = max(r, Tc[(i, j, s, k - 1)])
+        if e > 0:
+            r = max(r, G[(k, j, s, e - 1)][min(1, NG - 1)])
+        return r
+
+    def pkey(t):
+        if prio == "list":
+            return t[-1]
+        if t[0] == "P":
+            return (0, t[2], t[1])
+        return (1 if t[2] == t[1] + 1 else 2, t[1], t[2], t[4], t[3])
+
+    def place(t, t0):
+        if t[0] == "P":
+            _, i, k, _ = t
+            tt = t0
+            if k > 0:
+                tt = max([tt] + [Tc[(i, k, s, k - 1)] for s in range(ns)])
+            rr, rc, ee, fl = [0.0] * NG, [0.0] * NG, [0.0] * NG, [0.0] * NG
+            prev = (i - 1, k) if i > k else None
+            for g in range(NG):
+                gs = tt if g == 0 else ee[g - 1]
+                if prev:
+                    acc("panel Rr wait", Rr[prev][g] - gs)
+                    gs = max(gs, Rr[prev][g])
+                fct = max(prm["f"], fw) if world > 1 and g > 0 else prm["f"]
+                rr[g] = gs + prm["io_in"] + fct + prm["io_wb"]
+                rc[g] = rr[g] + prm["bt"] + prm["io_img"]
+                last = g + 1 == NG
+                ready = rc[g] + (fw if world > 1 and last else 0.0)
+                if prev:
+                    acc("panel Rt wait", E[prev][g] - ready)
+                ee[g] = (max(ready, E[prev][g]) if prev else ready) + prm["t"]
+                if world > 1:
+                    if last:
+                        fl[g] = ee[g] + hop
+                    if g > 0:
+                        fl[g - 1] = rr[g] - prm["io_wb"] + hop
+            Rr[(i, k)], Rc[(i, k)], E[(i, k)], FL[(i, k)] = rr, rc, ee, fl
+            return ee[-1]
+        _, k, j, s, e, i0, i1, _ = t
+        remote = world > 1 and owner_of(k, world, part) != owner_of(j, world, part)
+        rows = ([k] if e == 0 else []) + list(range(i0, i1))
+        tt = t0
+        pg = G[(k, j, s, e - 1)] if e > 0 else None
+        lastg = None
+        for idx, i in enumerate(rows):
+            if k > 0:
+                acc("chain Tc wait", Tc[(i, j, s, k - 1)] - tt)
+                tt = max(tt, Tc[(i, j, s, k - 1)])
+            tt += prm["e_ld"]
+            av = FL[(i, k)] if remote else Rc[(i, k)]
+            nxt = (FL if remote else Rc)[(rows[idx + 1], k)][0] if idx + 1 < len(rows) else 0.0
+            g_t = [0.0] * NG
+            for g in range(NG):
+                need = av[g + 1] if g + 1 < NG else nxt
+                st = max(tt, av[g], need)
+                if pg is not None and idx == 0:
+                    st = max(st, pg[min(g + 1, NG - 1)])
+                acc("chain wait inside" if (idx or g) else "chain wait at start", st - tt)
+                tt = st + prm["c"]
+                g_t[g] = tt
+            tt += prm["e_st"]
+            Tc[(i, j, s, k)] = tt
+            lastg = g_t
+        G[(k, j, s, e)] = lastg
+        return tt
+
+    workers = [[0.0] * W for _ in range(world)]
+    notready = [[] for _ in range(world)]  # (ready_time, n, task): dependencies placed
+    ready = [[] for _ in range(world)]     # (pkey, n, ready_time, task): startable
+    cnt = 0
+    for t in tasks:
+        if ndep[key(t)] == 0:
+            heapq.heappush(notready[rank_of(t)], (ready_time(t), cnt, t))
+            cnt += 1
+    left = len(tasks)
+    span = 0.0
+    while left:
+        # the rank whose earliest-free workgroup frees first (and has a known task)
+        best = None
+        for r in range(world):
+            if notready[r] or ready[r]:
+                tw = workers[r][0] + prm["disp"]
+                if best is None or tw < best[0]:
+                    best = (tw, r)
+        tw, r = best
+        while notready[r] and notready[r][0][0] <= tw:
+            rt, c, t = heapq.heappop(notready[r])
+            heapq.heappush(ready[r], (pkey(t), c, rt, t))
+        # the best startable task, else the one that can start soonest
+        if ready[r]:
+            _, _, rt, t = heapq.heappop(ready[r])
+        else:
+            rt, _, t = heapq.heappop(notready[r])
+        t0 = max(heapq.heappop(workers[r]) + prm["disp"], rt)
+        acc("idle (no startable task)", t0 - tw)
+        end = place(t, t0)
+        span = max(span, end)
+        heapq.heappush(workers[r], end)
+        left -= 1
+        for u in succ.get(key(t), []):
+            ndep[key(u)] -= 1
+            if ndep[key(u)] == 0:
+                heapq.heappush(notready[rank_of(u)], (ready_time(u), cnt, u))
+                cnt += 1
     return span
 
 
@@ -378,6 +573,22 @@ def main_dist(argv):
         for w in worlds[1:] if worlds[0] == 1 else worlds:
             tw = simulate_dist(items, M, N, w, mode=mode)
             print(f"  {mode:6s} forwarding, {w} GPUs: {tw / 1e3:7.1f} ms  S = {t1 / tw:5.2f}")
+    # what-if: column-granular member hand-off (fine = (df, dt) us)
+    for fine in ((4.0, 4.0), (2.0, 2.0)):
+        t1f = simulate_dist(items, M, N, 1, fine=fine)
+        line = f"  fine member hand-off {fine}: t1 {t1f / 1e3:6.1f} ms"
+        for w in worlds[1:] if worlds[0] == 1 else worlds:
+            tw = simulate_dist(items, M, N, w, fine=fine)
+            line += f", t{w} {tw / 1e3:6.1f} (S {t1f / tw:4.2f})"
+        print(line)
+    if os.environ.get("TQR_SIM_DYN", "1") == "1":
+        t1d = simulate_dist_dyn(items, M, N, 1)
+        print(f"  dependency-triggered dispatch (per-rank ready queues), 1 GPU: {t1d / 1e3:.1f} ms")
+        for pr in ("list", "class"):
+            for w in worlds[1:] if worlds[0] == 1 else worlds:
+                tw = simulate_dist_dyn(items, M, N, w, prio=pr)
+                print(f"  dyn/{pr:5s} {w} GPUs: {tw / 1e3:7.1f} ms  S = {t1 / tw:5.2f} (vs the in-order 1-GPU model)"
+                      f", {t1d / tw:5.2f} (vs dyn 1 GPU)")
     # the panel cost (factor, T, images, trailing, I/O) scale at which S(8) >= 6 (idle forwarding)
     for a in (1.0, 0.9, 0.8, 0.7, 0.6, 0.5, 0.4, 0.3):
         pp = dict(P, f=P["f"] * a, bt=P["bt"] * a, t=P["t"] * a, io_in=P["io_in"] * a, io_wb=P["io_wb"] * a,
