@@ -813,10 +813,22 @@ __device__ __forceinline__ void panel_step(double (&x)[IBX], double* Vs, double*
   const double Hm = TS ? (cw < IB ? Hs[C * TP + cw] : 0.0) : hrow[(C & 1) * 32 + cr];
   const double dc = readlane_d(Dm, 0);
   const double x0 = readlane_d(Hm, 0);
-  const double norm = sqrt(x0 * x0 + dc);
-  const double hd = x0 + (x0 >= 0.0 ? norm : -norm);
-  const double scale = norm != 0.0 ? rcp_nr(hd) : 1.0;
-  const double tau = 2.0 * rcp_nr(fma(scale * scale, dc, 1.0));
+  // norm, 1/norm from one reciprocal square root (two Newton steps), and tau = hd / (s norm) —
+  // LAPACK's form of 2 / |v|^2 (|v|^2 = 1 + dc / hd^2 = 2 s norm / hd): two independent
+  // reciprocals after the norm instead of a square root followed by two dependent reciprocals,
+  // ~10 fewer dependent fp64 operations per reflector step. norm == 0 keeps scale 1, tau 2.
+  const double n2 = fma(x0, x0, dc);
+  const bool z = n2 == 0.0;
+  const double h2 = 0.5 * n2;
+  double rn = __builtin_amdgcn_rsq(n2);
+  rn = rn * fma(-h2 * rn, rn, 1.5);
+  rn = rn * fma(-h2 * rn, rn, 1.5);
+  const double norm = z ? 0.0 : n2 * rn;
+  const double sg = x0 >= 0.0 ? 1.0 : -1.0;
+  const double hd = fma(sg, norm, x0);
+  const double scale = z ? 1.0 : rcp_nr(hd);
+  // (tau lies in [1, 2]; the product form can round an ulp outside)
+  const double tau = z ? 2.0 : fmin(fmax(hd * (sg * rn), 1.0), 2.0);
   const double fm = cw < IB ? tau * fma(scale, Dm, Hm) : 0.0;  // f_j for j = cw
   double* fb = wb + (w & 3) * 32;
   if (wr && w < 4) fb[cr] = fm;
