@@ -255,6 +255,15 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&clk, sizeof(unsigned long long) * 2 * 2 * ncu));
   CK(hipDeviceSynchronize());
   printf("%d CUs, %d elements per workgroup (tile rows streamed from HBM, ldm %ld)\n", ncu, nelem, LDM);
+  if (argc > 2 && atoi(argv[2]) == 1) {  // one wave per SIMD: what the I/O costs there
+    if (run<4, 32, 0, 1>("w4ib32", X, H, img, ncu, nelem, clk)) return 1;
+    if (run<4, 32, 1, 1>("w4ib32", X, H, img, ncu, nelem, clk)) return 1;
+    if (run<4, 32, 2, 1>("w4ib32", X, H, img, ncu, nelem, clk)) return 1;
+    if (run<4, 32, 3, 1>("w4ib32", X, H, img, ncu, nelem, clk)) return 1;
+    if (run<4, 32, 35, 1>("w4ib32", X, H, img, ncu, nelem, clk)) return 1;
+    if (run<8, 32, 2, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
+    return 0;
+  }
   if (run<8, 32, 0, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
   if (run<8, 32, 32, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
   if (run<8, 32, 40, 1>("w8ib32", X, H, img, ncu, nelem, clk)) return 1;
