@@ -426,7 +426,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
         // (written before the sync; wave-uniform: a scalar branch around the hooked phase 2 — as a
         // per-lane value the two apply32 bodies became exec-masked twins, and at NG == 1 that
         // broke the non-hooked one)
-        const bool pipe = NG > 1 && g + 1 == NG && uni(*(volatile int*)(sflag + 44)) != 0;
+        const bool pipe = NG > 1 && g + 1 == NG && uni(lds_ld_volatile(sflag + 44)) != 0;
 #ifdef TQR_FLOW_STAMPS
         GTR(3, __builtin_amdgcn_s_memrealtime());
 #endif
