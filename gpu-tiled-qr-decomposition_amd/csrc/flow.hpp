@@ -1,12 +1,14 @@
-// Persistent dataflow engine ("flow"): one 256-thread workgroup per CU pulls tasks from a
-// statically ordered list (atomic dequeue) and synchronises with other workgroups only through
-// monotone progress counters in global memory (agent-scope release / acquire, CDNA4 recipe of
-// MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility").
+// Persistent dataflow engine ("flow"): one 512-thread workgroup per CU (engine shape ShapeW8;
+// ShapeW4: two 256-thread workgroups) pulls tasks from a statically ordered list (atomic dequeue)
+// and synchronises with other workgroups only through monotone progress counters in global memory
+// (write-through stores drained before one lane's counter add, L1-bypassing loads after the poll:
+// MI355X_MICROARCH.md "Workgroup dispatch ... inter-workgroup visibility", first table row).
 //
 // Tasks (the reference DAG of src/gridscheduler.c, regrouped):
 //   QRS(k)          GEQRT of tile (k,k), reflector group by group;
 //   QRD(i,k)        TSQRT of [R_kk; tile (i,k)], group by group;
-//   CHAIN(k,j,s,e)  one 64-column strip s of tile column j at step k: segment e of the chain
+//   CHAIN(k,j,s,e)  one 128-column strip s of tile column j at step k (ShapeW4: 64 columns):
+//                   segment e of the chain
 //                   UNMQR(k,j) (segment 0 only), TSMQR(i,j,k) for i in [i0,i1). The strip of
 //                   tile (k,j) (the TSMQR head rows) stays owned by the chain across elements.
 // Progress counters (zeroed per factorisation):
