@@ -1732,14 +1732,13 @@ static int geqrt_host_flow(tqr_plan* pl, void* A, void* tau, int ldm, size_t es)
   auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t0 = now();
   std::atomic<long long> t_up{0}, t_dn{0};
-  if (verbose) HIPCHK(hipEventRecord(pl->ev0, s));
-  if ((st = plan_execute_serial(pl, pl->hA, m, pl->hT, s, &xa))) {
-    (void)hipStreamSynchronize(s);
-    return st;
-  }
-  if (verbose) HIPCHK(hipEventRecord(pl->ev1, s));
-  // host side, while the launch runs: nu threads stage tile columns in order (the last one to
-  // finish a column flags it), nd threads move finished chunks back to the caller's array
+  // host side, beside the launch: nu threads stage tile columns in order (the last one to finish a
+  // column flags it), nd threads move finished chunks back to the caller's array. They start
+  // BEFORE the launch call: the launched kernel waits for the staging flags, so the staging must
+  // not depend on this thread returning from HIP calls (another thread's hipFree — e.g. a
+  // concurrent tqr_cache_clear — waits for the device to be idle, i.e. for this kernel; a staging
+  // started behind a HIP call stalled by it would leave the kernel waiting until its timeout)
+  std::atomic<int> launched{0};
   const int nthr = host_threads();
   const int nu = std::max(1, nthr / 2), nd = std::max(1, nthr - nu);
   const size_t col = es * (size_t)m;
@@ -1768,7 +1767,7 @@ static int geqrt_host_flow(tqr_plan* pl, void* A, void* tau, int ldm, size_t es)
           for (long spins = 0; __atomic_load_n(&hdn[(size_t)j * nxc + c], __ATOMIC_ACQUIRE) < gen; ++spins) {
             if (failed.load(std::memory_order_relaxed)) return;
             if ((spins & 255) == 255) {
-              if (hipStreamQuery(s) != hipErrorNotReady &&
+              if (launched.load(std::memory_order_acquire) && hipStreamQuery(s) != hipErrorNotReady &&
                   __atomic_load_n(&hdn[(size_t)j * nxc + c], __ATOMIC_ACQUIRE) < gen) {
                 failed.store(1);
                 return;
@@ -1783,7 +1782,29 @@ static int geqrt_host_flow(tqr_plan* pl, void* A, void* tau, int ldm, size_t es)
       }
       if (verbose) t_dn.store(std::max<long long>(t_dn.load(), (long long)((now() - t0) * 1e3)));
     });
-  run_jobs(jobs);
+  std::vector<std::thread> th;
+  std::vector<size_t> inline_jobs;  // jobs whose thread could not be created: run after the launch
+  for (size_t x = 0; x < jobs.size(); ++x) {
+    try {
+      th.emplace_back(jobs[x]);
+    } catch (...) {
+      inline_jobs.push_back(x);
+    }
+  }
+  if (verbose) (void)hipEventRecord(pl->ev0, s);
+  st = plan_execute_serial(pl, pl->hA, m, pl->hT, s, &xa);
+  if (st == TQR_OK) {
+    if (verbose) (void)hipEventRecord(pl->ev1, s);
+    launched.store(1, std::memory_order_release);
+  } else {
+    failed.store(1);  // (the copy-out threads stop waiting)
+  }
+  for (size_t x : inline_jobs) jobs[x]();
+  for (auto& t : th) t.join();
+  if (st != TQR_OK) {
+    (void)hipStreamSynchronize(s);
+    return st;
+  }
   st = tqr_plan_status(pl, s);
   if (st == TQR_OK && failed.load()) st = TQR_EHIP;
   if (verbose && st == TQR_OK) {

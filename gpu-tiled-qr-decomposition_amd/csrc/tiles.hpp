@@ -710,7 +710,7 @@ __device__ __forceinline__ void dpp_halve(const double* v, double* out, bool up)
 template <int N>
 struct RS {
   __device__ static __forceinline__ double run(double (&v)[N], int lane) {
-    static_assert(N == 32 || N == 16, "IB must be 16 or 32");
+    static_assert(N == 32 || N == 16 || N == 8, "window of 8, 16 or 32 columns");
     constexpr int H1 = N / 2, H2 = N / 4, H3 = N / 8;
 #pragma unroll
     for (int i = 0; i < H1; ++i) {
@@ -733,6 +733,10 @@ struct RS {
       double d1[1];
       dpp_halve<DPP_QUAD_3210, 1>(d2, d1, lane & 2);
       e = d1[0];
+    } else if constexpr (N == 8) {
+      e = c[0];
+      e += dpp<DPP_ROW_HALF_MIRROR>(e);
+      e += dpp<DPP_QUAD_3210>(e);
     } else {
       double d1[1];
       dpp_halve<DPP_ROW_HALF_MIRROR, 1>(c, d1, lane & 4);
@@ -907,13 +911,18 @@ __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, 
 #pragma unroll
     for (int j = 0; j < IB; ++j) hrow[j] = x[j];
   }
-  // reduce the live window only: all IB columns while more than IB/2 are live, then the half
-  constexpr int HALF = IB == 32 ? 16 : IB;
+  // reduce the live window only: all IB columns while more than IB/2 are live, then the half,
+  // then (IB = 32) the quarter for the last 8 reflectors
+  constexpr int HALF = IB == 32 ? 16 : IB, Q3 = IB == 32 ? 24 : IB;
 #pragma clang loop unroll(disable)
   for (int C = 0; C < HALF; ++C) panel_step<B, TS, IB, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
   if constexpr (HALF < IB) {
 #pragma clang loop unroll(disable)
-    for (int C = HALF; C < IB; ++C) panel_step<B, TS, IB / 2, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
+    for (int C = HALF; C < Q3; ++C) panel_step<B, TS, IB / 2, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
+  }
+  if constexpr (Q3 < IB) {
+#pragma clang loop unroll(disable)
+    for (int C = Q3; C < IB; ++C) panel_step<B, TS, IB / 4, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
   }
   __syncthreads();
   if (TS) {
