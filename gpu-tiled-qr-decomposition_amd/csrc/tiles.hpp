@@ -66,6 +66,31 @@ extern __device__ unsigned long long g_bt[8];
 #else
 #define BT_STAMP(i) do {} while (0)
 #endif
+// reflector-step phase stamps (tools/ubench/panel_bench.hip built with -DTQR_PS_STAMPS only):
+// per step, s_memtime deltas summed in registers, added to g_ps at the end of the group
+#ifdef TQR_PS_STAMPS
+extern __device__ unsigned long long g_ps[8];
+#define PS_DECL unsigned long long ps_acc_[6] = {0, 0, 0, 0, 0, 0}, ps_t_ = 0;
+#define PS_MARK(i)                                                   \
+  do {                                                               \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime();      \
+    if ((i) > 0) ps_acc_[(i) - 1] += n_ - ps_t_;                     \
+    ps_t_ = n_;                                                      \
+  } while (0)
+#define PS_ARGS , ps_acc_, ps_t_
+#define PS_PARAMS , unsigned long long (&ps_acc_)[6], unsigned long long& ps_t_
+#define PS_FLUSH()                                                                   \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x == 0)                                         \
+      for (int i_ = 0; i_ < 6; ++i_) atomicAdd(&g_ps[i_], ps_acc_[i_]);              \
+  } while (0)
+#else
+#define PS_DECL
+#define PS_MARK(i) do {} while (0)
+#define PS_ARGS
+#define PS_PARAMS
+#define PS_FLUSH() do {} while (0)
+#endif
 
 constexpr int NT = 256;  // threads per workgroup (4 waves)
 
@@ -794,13 +819,14 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 //   5. rows update x_j -= f_j v (tails) / head_j -= f_j (GE head row, TS head in `hout`).
 template <int B, bool TS, int NW, int IBX = Geo<B>::IB>
 __device__ __forceinline__ void panel_step(double (&x)[IBX], double* Vs, double* Hs, double* tauv, double* red,
-                                           double* wb, double* hrow, double* hout, int c0, int C, bool own, int rt) {
+                                           double* wb, double* hrow, double* hout, int c0, int C, bool own, int rt PS_PARAMS) {
   using g = Geo<B, IBX>;
   constexpr int IB = g::IB, TP = g::TP, VP = g::VP;
   constexpr int SPAN = 64 / NW;  // lanes holding the same column after reduce-scatter
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int rc = c0 + C;  // GE: tile row of the reflector head
   const bool tail = own && (TS || rt > rc);  // rt: the tile row this thread holds
+  PS_MARK(0);
   double pv[NW];
   const double xm = tail ? x[0] : 0.0;  // one select, not one per product (GE: 64 v_cndmask)
 #pragma unroll
@@ -811,12 +837,14 @@ __device__ __forceinline__ void panel_step(double (&x)[IBX], double* Vs, double*
   const bool wr = (lane & (SPAN - 1)) == 0;
   double* rb = red + (C & 1) * 128;
   if (wr && w < 4) rb[w * 32 + cr] = ws;  // rows live in waves 0-3
+  PS_MARK(1);
   // (GE: the head row reached hrow at the end of the previous step, off this barrier's path)
   __syncthreads();
   const double Dm = (rb[cr] + rb[32 + cr]) + (rb[64 + cr] + rb[96 + cr]);
   const double Hm = TS ? (cw < IB ? Hs[C * TP + cw] : 0.0) : hrow[(C & 1) * 32 + cr];
   const double dc = readlane_d(Dm, 0);
   const double x0 = readlane_d(Hm, 0);
+  PS_MARK(2);
   // norm, 1/norm from one reciprocal square root (two Newton steps), and tau = hd / (s norm) —
   // LAPACK's form of 2 / |v|^2 (|v|^2 = 1 + dc / hd^2 = 2 s norm / hd): two independent
   // reciprocals after the norm instead of a square root followed by two dependent reciprocals,
@@ -834,6 +862,7 @@ __device__ __forceinline__ void panel_step(double (&x)[IBX], double* Vs, double*
   // (tau lies in [1, 2]; the product form can round an ulp outside)
   const double tau = z ? 2.0 : fmin(fmax(hd * (sg * rn), 1.0), 2.0);
   const double fm = cw < IB ? tau * fma(scale, Dm, Hm) : 0.0;  // f_j for j = cw
+  PS_MARK(3);
   double* fb = wb + (w & 3) * 32;
   if (wr && w < 4) fb[cr] = fm;
   if (TS && w == 0 && wr && cw < IB) hout[C * TP + cw] = Hm - fm;  // cw == C: R_CC = x0 - f_C
@@ -846,6 +875,7 @@ __device__ __forceinline__ void panel_step(double (&x)[IBX], double* Vs, double*
     f[2 * h] = v2.x;
     f[2 * h + 1] = v2.y;
   }
+  PS_MARK(4);
   // branch-free update (a divergent tail/head-row branch made the wave holding the GE head row
   // run both streams): tails x_j -= f_j (scale x_C), the GE head row x_j -= f_j (coefficient 1,
   // the same rounding as a subtraction), all other rows coefficient 0 (x_j unchanged)
@@ -868,6 +898,7 @@ __device__ __forceinline__ void panel_step(double (&x)[IBX], double* Vs, double*
 #pragma unroll
     for (int h = 0; h < NW / 2; ++h) hb[h] = make_double2(x[2 * h], x[2 * h + 1]);
   }
+  PS_MARK(5);
 }
 
 // Work for the waves without panel rows (multi-GPU: forwarding the previous reflector group's
@@ -914,16 +945,18 @@ __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, 
   // reduce the live window only: all IB columns while more than IB/2 are live, then the half,
   // then (IB = 32) the quarter for the last 8 reflectors
   constexpr int HALF = IB == 32 ? 16 : IB, Q3 = IB == 32 ? 24 : IB;
+  PS_DECL
 #pragma clang loop unroll(disable)
-  for (int C = 0; C < HALF; ++C) panel_step<B, TS, IB, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
+  for (int C = 0; C < HALF; ++C) panel_step<B, TS, IB, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt PS_ARGS);
   if constexpr (HALF < IB) {
 #pragma clang loop unroll(disable)
-    for (int C = HALF; C < Q3; ++C) panel_step<B, TS, IB / 2, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
+    for (int C = HALF; C < Q3; ++C) panel_step<B, TS, IB / 2, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt PS_ARGS);
   }
   if constexpr (Q3 < IB) {
 #pragma clang loop unroll(disable)
-    for (int C = Q3; C < IB; ++C) panel_step<B, TS, IB / 4, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt);
+    for (int C = Q3; C < IB; ++C) panel_step<B, TS, IB / 4, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt PS_ARGS);
   }
+  PS_FLUSH();
   __syncthreads();
   if (TS) {
     for (int idx = t; idx < IB * IB; idx += 256) {

@@ -6,6 +6,9 @@
 #define TQR_BT_STAMPS
 #include "tiles.hpp"
 namespace tqr { __device__ unsigned long long g_bt[8]; }
+#ifdef TQR_PS_STAMPS
+namespace tqr { __device__ unsigned long long g_ps[8]; }
+#endif
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 using namespace tqr;
 constexpr int B = 256;
@@ -86,6 +89,12 @@ static int run(const char* name, double* out, int blocks) {
   k_panel<TS, NTH><<<blocks, NTH, lds>>>(out, 4);
   CK(hipDeviceSynchronize());
   float ms;
+#ifdef TQR_PS_STAMPS
+  {
+    unsigned long long z[8] = {0};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(tqr::g_ps), z, sizeof(z)));
+  }
+#endif
   CK(hipEventRecord(e0));
   k_panel<TS, NTH><<<blocks, NTH, lds>>>(out, iters);
   CK(hipEventRecord(e1));
@@ -93,6 +102,16 @@ static int run(const char* name, double* out, int blocks) {
   CK(hipEventElapsedTime(&ms, e0, e1));
   printf("%-8s %3d threads: %7.2f us per group (%5.3f us per reflector)\n", name, NTH, ms * 1e3 / iters,
          ms * 1e3 / iters / G::IB);
+#ifdef TQR_PS_STAMPS
+  unsigned long long ps[8];
+  CK(hipMemcpyFromSymbol(ps, HIP_SYMBOL(tqr::g_ps), sizeof(ps)));
+  double tot = 0;
+  for (int i = 0; i < 5; ++i) tot += (double)ps[i];
+  const double per = tot / (iters * (double)G::IB);  // s_memtime ticks per reflector step (wave 0 of block 0)
+  printf("   step phases (wave 0, %.0f ticks per step): products+reduce %.0f%%, barrier+sums %.0f%%, scalar %.0f%%, "
+         "f broadcast %.0f%%, update+shift %.0f%%\n", per, 100 * ps[0] / tot, 100 * ps[1] / tot, 100 * ps[2] / tot,
+         100 * ps[3] / tot, 100 * ps[4] / tot);
+#endif
   return 0;
 }
 
