@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 4: TSQRT panel in the column layout (panel_ts_cols) — ubench, parity, A/B c3 / c5.
+set -o pipefail
+OUT=gpurun_out/${1:-r4tscols}
+mkdir -p $OUT
+timeout -k 10 120 ./tools/ubench/panel_bench_cols > $OUT/panel_bench_cols.txt 2>&1 || { echo "ubench failed"; exit 1; }
+head -12 $OUT/panel_bench_cols.txt
+timeout -k 10 900 python -u -m pytest -q -x -m gpu --timeout 120 --timeout-method thread tests > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+bash tools/ab_bench.sh $OUT/ab_f64 2 libtqr_base.so libtqr.so || exit 1
+BENCH_ARGS="--storage f32 --rows 32768 --cols 32768" bash tools/ab_bench.sh $OUT/ab_f32 2 libtqr_base.so libtqr.so || exit 1
