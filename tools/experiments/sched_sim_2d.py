@@ -2,7 +2,7 @@
 instead of following their tile column's owner, every cross-rank strip / head-row hand-over
 charged a flag hop plus a 256 KiB xGMI copy. Usage: python tools/sched_sim_2d.py [M] [N]"""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # tools/
 import sched_sim as S
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 64

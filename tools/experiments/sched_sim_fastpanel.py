@@ -2,7 +2,7 @@
 in-order per-rank dequeue and under dependency-triggered dispatch (simulate_dist_dyn), 1 and 8
 ranks. Usage: python tools/sched_sim_fastpanel.py [M] [N] [a ...]"""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # tools/
 import sched_sim as S
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 64

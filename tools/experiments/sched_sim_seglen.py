@@ -3,7 +3,7 @@ makespan and S(world) per segment length, with a per-segment cost (TQR_SIM_SEG u
 calibrated on one MI355X, 65536x16384 at segment length 2 vs 8 = 635.3 vs 607.6 ms, i.e. 27.7 ms
 for ~356k extra segments on 256 workgroups). Usage: python tools/sched_sim_seglen.py [M] [N] [seglen ...]"""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # tools/
 import sched_sim as S
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 64

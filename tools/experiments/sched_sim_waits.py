@@ -1,5 +1,5 @@
 import sys, os
-sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))  # tools/
 import sched_sim as S
 items = S.export_list(256, 64)
 for w in (1, 8):

@@ -4,7 +4,7 @@ its chains) dequeued only by the 32 workgroups of XCD x(j) (the multi-GPU partit
 could be stored write-back into that XCD's L2 instead of write-through (a cheaper element
 hand-over: e_ld / e_st scaled by `h`). Usage: python tools/sched_sim_xcd.py [M] [N] [h ...]"""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # tools/
 import sched_sim as S
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 64
