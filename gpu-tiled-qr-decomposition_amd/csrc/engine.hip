@@ -473,19 +473,38 @@ struct XferPlan {
 //   la_tail    the last la_tail steps (TQR_LA_TAIL): their lookahead column runs one element per
 //              segment, so the element that finishes the next diagonal tile runs beside the UNMQR
 //              element instead of behind it
+//   tail       the last `tail` steps (TQR_TAIL; default: default_tail): every chain tail_sl elements
+//              per segment (TQR_TAIL_SEGLEN, default 1)
 //   Tg         the estimator's panel group-step cost in chain elements (TQR_TG, default 1.4)
 //   lazy       TQR_LAZY (default 1), la / lac: TQR_LA / TQR_LAC (see build_flow_plan)
 struct FlowKnobs {
-  int seglen = 8, seglen_la = 8, la_tail = 0;
+  int seglen = 8, seglen_la = 8, la_tail = 0, tail = 0, tail_sl = 1;
   double Tg = 1.4, lazy = 1.0, la = 0.0, lac = 0.0;
 };
-static FlowKnobs knobs_from_env(int seglen) {
+// Default tail (fp64 storage): the steps whose columns have at most kTailRows rows below the
+// diagonal, i.e. whose chains are short and on the critical path. One element per segment lets a
+// column's elements run on different workgroups, pipelined group by group through the head rows
+// (Ac), instead of one after the other in one workgroup. Measured at 16384^2 (64 steps): tail 32
+// 122.7-122.8 ms against 124.7-124.9 (24: 124.0, 40: 122.9-123.3, 48: 124.2-124.3; profiles/r04/
+// tail/). fp32 storage keeps its head strip in registers across a segment, so one-element segments
+// add a head load and store per element there: no gain at 16-32 steps of 128, slower beyond
+// (48: +2.3 ms) — off for fp32. Tall matrices (65536 x 16384) never reach the tail rows.
+constexpr int kTailRows = 31;
+static int default_tail(int p, int q, int dtype) {
+  const int kmax = std::min(p, q);
+  if (dtype != TQR_F64) return 0;
+  return std::max(0, std::min(kmax, kmax - (p - 1 - kTailRows)));
+}
+static FlowKnobs knobs_from_env(int seglen, int tail_default = 0) {
   FlowKnobs kn;
   kn.seglen = std::max(1, seglen);
+  kn.tail = tail_default;
   const char* esl = getenv("TQR_SEGLEN_LA");
   kn.seglen_la = esl ? std::max(1, atoi(esl)) : kn.seglen;
   const char* e = getenv("TQR_LA_TAIL");
   kn.la_tail = e ? std::max(0, atoi(e)) : 0;
+  if (const char* et = getenv("TQR_TAIL")) kn.tail = std::max(0, atoi(et));
+  if (const char* ets = getenv("TQR_TAIL_SEGLEN")) kn.tail_sl = std::max(1, atoi(ets));
   if (const char* eg = getenv("TQR_TG")) kn.Tg = atof(eg);
   if (const char* el = getenv("TQR_LAZY")) kn.lazy = atof(el);
   if (const char* ela = getenv("TQR_LA")) kn.la = atof(ela);
@@ -513,7 +532,7 @@ static void build_flow_plan(int p, int q, int ns, int ng, const FlowKnobs& kn, F
   const int kmax = std::min(p, q);
   // segment length per chain: shorter segments for the lookahead column pipeline consecutive
   // elements on different workgroups at reflector-group granularity
-  auto seglen_of = [&](int k, int j) { return seglen_of_chain(k, j, kmax, kn.seglen, kn.seglen_la, kn.la_tail); };
+  auto seglen_of = [&](int k, int j) { return seglen_of_chain(k, j, kmax, kn.seglen, kn.seglen_la, kn.la_tail, kn.tail, kn.tail_sl); };
   // host-pointer API: tile column j arrives (uploaded) at arrive(j); step-0 tasks start after it
   const bool xfer = xp && xp->nxc > 0;
   auto arrive = [&](int j) { return xfer ? (j + 1) * xp->tcol : 0.0; };
@@ -973,7 +992,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     pl->grid = full_grid;
     if (const char* gs = getenv("TQR_FLOW_GRID")) pl->grid = std::max(1, atoi(gs));
     FlowPlan fp;
-    pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid));
+    pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid), default_tail(pl->p, pl->q, dtype));
     build_flow_plan(pl->p, pl->q, pl->ns, pl->ng, pl->knobs, fp);
     pl->nflow_global = (int)fp.items.size();
     if (world > 1) partition_flow_plan(fp, rank, world);
@@ -1045,9 +1064,10 @@ int tqr_plan_status(tqr_plan* pl, void* stream) {
 static constexpr size_t kBusIdBytes = 64;
 // a rank's handle: PCI bus id, the task-list signature (every rank must partition the same global
 // list: segment lengths, lookahead tail, list length), the IPC handles of Rf and the workspaces
-constexpr size_t kSigInts = 4;
+constexpr size_t kSigInts = 6;
 static void plan_signature(const tqr_plan* pl, int* sig) {
   sig[0] = pl->knobs.seglen; sig[1] = pl->knobs.seglen_la; sig[2] = pl->knobs.la_tail; sig[3] = pl->nflow_global;
+  sig[4] = pl->knobs.tail; sig[5] = pl->knobs.tail_sl;
 }
 size_t tqr_dist_handle_bytes(const tqr_plan* pl) {
   return pl ? kBusIdBytes + sizeof(int) * kSigInts + sizeof(hipIpcMemHandle_t) * (1 + (size_t)pl->kmax) : 0;
@@ -1124,8 +1144,10 @@ int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
     plan_signature(pl, mine);
     if (memcmp(sig, mine, sizeof(sig)) != 0) {  // a launch over different lists would deadlock
       fprintf(stderr, "tqr: rank %d and rank %d built different task lists (segment lengths %d/%d vs %d/%d, "
-              "lookahead tail %d vs %d, %d vs %d tasks): set TQR_SEGLEN / TQR_FLOW_GRID alike on every rank\n",
-              pl->rank, r, mine[0], mine[1], sig[0], sig[1], mine[2], sig[2], mine[3], sig[3]);
+              "lookahead tail %d vs %d, tail %d/%d vs %d/%d, %d vs %d tasks): set TQR_SEGLEN / TQR_TAIL / "
+              "TQR_FLOW_GRID alike on every rank\n",
+              pl->rank, r, mine[0], mine[1], sig[0], sig[1], mine[2], sig[2], mine[4], mine[5], sig[4], sig[5],
+              mine[3], sig[3]);
       close_opened(pl);
       return TQR_EINVAL;
     }
@@ -1192,7 +1214,7 @@ int tqr_dist_owner(const tqr_plan* pl, int tile_col) {
 // Host-only task-list helpers below describe the fp64 engine's list (flow_shape(TQR_F64)).
 static void host_flow_plan(int M, int N, int b, int seglen, FlowPlan& fp, const XferPlan* xp = nullptr) {
   const int sh = flow_shape(TQR_F64);
-  build_flow_plan(M, N, shape_ns(sh, b), b / shape_ib(sh, b), knobs_from_env(seglen), fp, xp);
+  build_flow_plan(M, N, shape_ns(sh, b), b / shape_ib(sh, b), knobs_from_env(seglen, default_tail(M, N, TQR_F64)), fp, xp);
 }
 int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1 || world < 1 || rank < 0 || rank >= world) return TQR_EINVAL;
@@ -1342,6 +1364,7 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     f.rf_done = (long)pl->kmax * pl->p * pl->ng;
     f.epoch = pl->world > 1 ? ++pl->epoch : 0;
     f.seglen = pl->knobs.seglen; f.seglen_la = pl->knobs.seglen_la; f.la_tail = pl->knobs.la_tail;
+    f.tail = pl->knobs.tail; f.tail_sl = pl->knobs.tail_sl;
     if (xa) {
       f.hsrc = xa->hsrc; f.hdst = xa->hdst; f.hld = xa->hld; f.hup = xa->hup; f.hdn = xa->hdn; f.gen = xa->gen;
       f.Uc = f.Rr + (size_t)pl->kmax * pl->ng;

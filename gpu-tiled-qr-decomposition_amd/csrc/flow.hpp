@@ -236,7 +236,7 @@ struct FlowArgs {
   int* hup;
   int* hdn;
   int* Uc;
-  int gen, nxc, xrows, seglen, seglen_la, la_tail;
+  int gen, nxc, xrows, seglen, seglen_la, la_tail, tail, tail_sl;
   // storage of the tile columns: global tile column j is local column j / cdiv of A (and tau
   // column k of panel k local column k / cdiv). Single GPU: cdiv = 1. Multi-GPU: cdiv = world —
   // a rank stores only the tile columns it owns (one per block of `world` consecutive columns,
@@ -255,9 +255,14 @@ __host__ __device__ inline int tile_owner(int j, int world, int cyclic = 0) {
   return (blk & 1) ? world - 1 - r : r;
 }
 
-// Segment length of chain (k, j): the lookahead column (j = k+1) may use its own (seglen_la), and
-// the last la_tail steps' lookahead column one element per segment (engine.hip la_tail_of).
-__host__ __device__ inline int seglen_of_chain(int k, int j, int kmax, int seglen, int seglen_la, int la_tail) {
+// Segment length of chain (k, j): the last `tail` steps' chains tail_sl elements per segment (their
+// elements then pipeline group by group over workgroups instead of running one after the other in
+// one: the factorisation's tail is a few short columns per step on the critical path); else the
+// lookahead column (j = k+1) may use its own (seglen_la), and the last la_tail steps' lookahead
+// column one element per segment (engine.hip FlowKnobs).
+__host__ __device__ inline int seglen_of_chain(int k, int j, int kmax, int seglen, int seglen_la, int la_tail,
+                                               int tail = 0, int tail_sl = 1) {
+  if (k >= kmax - tail) return tail_sl;
   if (j != k + 1) return seglen;
   return k >= kmax - la_tail ? 1 : seglen_la;
 }

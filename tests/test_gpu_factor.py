@@ -247,8 +247,9 @@ def test_legacy_entry_points(tqr, oracle):
 
 def test_task_order_and_lookahead_segments_bitexact(tqr):
     """The persistent engine computes the same bits whatever valid task order it runs: the plan's
-    estimated order vs a step-major permutation loaded with tqr_plan_set_tasks, and vs a plan whose
-    lookahead column uses other segment lengths (TQR_SEGLEN_LA, read at plan creation)."""
+    estimated order vs a step-major permutation loaded with tqr_plan_set_tasks, and vs plans whose
+    lookahead column or tail steps use other segment lengths (TQR_SEGLEN_LA, TQR_TAIL,
+    TQR_TAIL_SEGLEN, read at plan creation)."""
     import ctypes
     import torch
     from test_capi import step_major
@@ -285,3 +286,18 @@ def test_task_order_and_lookahead_segments_bitexact(tqr):
             os.environ["TQR_SEGLEN_LA"] = old
     A2, t2 = run(p2)
     assert torch.equal(A0, A2) and torch.equal(t0, t2)
+    # the fp64 list's one-element tail segments (engine.hip default_tail; every step of this size)
+    # against none (TQR_TAIL=0) and two-element ones
+    for env in ({"TQR_TAIL": "0"}, {"TQR_TAIL_SEGLEN": "2"}):
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            p3 = tqr.TiledQR(m, n, b, torch.float64)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k)
+                else:
+                    os.environ[k] = v
+        A3, t3 = run(p3)
+        assert torch.equal(A0, A3) and torch.equal(t0, t3), env

@@ -87,6 +87,10 @@ def test_flow_plan_topological(tqr, M, N, b, seg):
     assert sw in (64, 128)
     ns = (b + sw - 1) // sw
     panels = sum(M - k for k in range(kmax))
-    chains = sum((N - k - 1) * ns * max(1, -(-(M - k - 1) // seg)) for k in range(kmax))
+    # fp64 list: the last `tail` steps (columns with <= 31 rows below the diagonal) run one-element
+    # segments (engine.hip default_tail)
+    tail = max(0, min(kmax, kmax - (M - 1 - 31)))
+    sl = lambda k: 1 if k >= kmax - tail else seg
+    chains = sum((N - k - 1) * ns * max(1, -(-(M - k - 1) // sl(k))) for k in range(kmax))
     assert n.value == panels + chains
     assert o.value == 1
