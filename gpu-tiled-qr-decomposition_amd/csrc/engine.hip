@@ -476,7 +476,8 @@ struct XferPlan {
 //   tail       the last `tail` steps (TQR_TAIL; default: default_tail): every chain tail_sl elements
 //              per segment (TQR_TAIL_SEGLEN, default 1)
 //   Tg         the estimator's panel group-step cost in chain elements (TQR_TG, default 1.4)
-//   lazy       TQR_LAZY (default 1), la / lac: TQR_LA / TQR_LAC (see build_flow_plan)
+//   lazy       TQR_LAZY (default 1), la / lac: TQR_LA (default: default_la) / TQR_LAC (see
+//              build_flow_plan)
 struct FlowKnobs {
   int seglen = 8, seglen_la = 8, la_tail = 0, tail = 0, tail_sl = 1;
   double Tg = 1.4, lazy = 1.0, la = 0.0, lac = 0.0;
@@ -495,10 +496,16 @@ static int default_tail(int p, int q, int dtype) {
   if (dtype != TQR_F64) return 0;
   return std::max(0, std::min(kmax, kmax - (p - 1 - kTailRows)));
 }
-static FlowKnobs knobs_from_env(int seglen, int tail_default = 0) {
+// Default panel lookahead (TQR_LA, chain elements): 2 for fp32 storage, whose run is paced by the
+// panel groups (c5 465.8-466.4 vs 467.2-467.3 ms, two alternating rounds; 4: 466.2-466.5, 6:
+// 467.7; round 4's earlier 4 vs 0: 469.0-469.1 vs 470.4-470.7), 0 for fp64 (2: +0.1-0.2 ms;
+// profiles/r04/la_f32/).
+static double default_la(int dtype) { return dtype == TQR_F32 ? 2.0 : 0.0; }
+static FlowKnobs knobs_from_env(int seglen, int tail_default = 0, double la_default = 0.0) {
   FlowKnobs kn;
   kn.seglen = std::max(1, seglen);
   kn.tail = tail_default;
+  kn.la = la_default;
   const char* esl = getenv("TQR_SEGLEN_LA");
   kn.seglen_la = esl ? std::max(1, atoi(esl)) : kn.seglen;
   const char* e = getenv("TQR_LA_TAIL");
@@ -992,7 +999,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     pl->grid = full_grid;
     if (const char* gs = getenv("TQR_FLOW_GRID")) pl->grid = std::max(1, atoi(gs));
     FlowPlan fp;
-    pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid), default_tail(pl->p, pl->q, dtype));
+    pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid), default_tail(pl->p, pl->q, dtype), default_la(dtype));
     build_flow_plan(pl->p, pl->q, pl->ns, pl->ng, pl->knobs, fp);
     pl->nflow_global = (int)fp.items.size();
     if (world > 1) partition_flow_plan(fp, rank, world);
