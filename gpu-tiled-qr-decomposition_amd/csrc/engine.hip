@@ -766,6 +766,7 @@ struct tqr_plan {
   kfn kp = nullptr, ku = nullptr;
   size_t ldsP = 0, ldsU = 0;
   int profile = 0;
+  int chain_asm = 1;  // fp64 chains on the hand-scheduled MFMA stream (TQR_CHAIN_ASM=0: compiler-scheduled)
   // flow engine
   int engine = 1;          // 1 = persistent dataflow (default), 0 = wave-batched launches
   Item* d_flow = nullptr;
@@ -1000,6 +1001,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (const char* gs = getenv("TQR_FLOW_GRID")) pl->grid = std::max(1, atoi(gs));
     FlowPlan fp;
     pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid), default_tail(pl->p, pl->q, dtype), default_la(dtype));
+    if (const char* eca = getenv("TQR_CHAIN_ASM")) pl->chain_asm = atoi(eca) != 0;
     build_flow_plan(pl->p, pl->q, pl->ns, pl->ng, pl->knobs, fp);
     pl->nflow_global = (int)fp.items.size();
     if (world > 1) partition_flow_plan(fp, rank, world);
@@ -1369,7 +1371,10 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     f.dist = pl->world > 1; f.rank = pl->rank; f.world = pl->world; f.cyclic = pl->cyclic; f.peers = pl->d_peers; f.Rf = pl->d_rf;
     f.cdiv = pl->world;  // multi-GPU: the rank's own tile columns only, packed (FlowArgs::cdiv)
     f.rf_done = (long)pl->kmax * pl->p * pl->ng;
-    f.epoch = pl->world > 1 ? ++pl->epoch : 0;
+    // the launch's epoch: committed to the plan only once the launch is enqueued (a failed
+    // enqueue must not leave this rank one epoch ahead of its peers for good)
+    f.epoch = pl->world > 1 ? pl->epoch + 1 : 0;
+    f.chain_asm = pl->chain_asm;
     f.seglen = pl->knobs.seglen; f.seglen_la = pl->knobs.seglen_la; f.la_tail = pl->knobs.la_tail;
     f.tail = pl->knobs.tail; f.tail_sl = pl->knobs.tail_sl;
     if (xa) {
@@ -1385,6 +1390,7 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
     hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(pl->nt), pl->ldsF, cs, f);
     HIPCHK(hipGetLastError());
+    if (pl->world > 1) pl->epoch = f.epoch;
     if (pl->profile) {
       HIPCHK(hipEventRecord(pl->ev1, cs));
       HIPCHK(hipEventSynchronize(pl->ev1));

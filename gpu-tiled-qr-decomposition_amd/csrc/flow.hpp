@@ -242,6 +242,9 @@ struct FlowArgs {
   // a rank stores only the tile columns it owns (one per block of `world` consecutive columns,
   // in the snake and the cyclic partition alike), packed in column order.
   int cdiv;
+  // fp64 chains of 128- and 256-tiles on the hand-scheduled MFMA stream (chain_asm.hpp); 0: the
+  // compiler-scheduled flow_chain (TQR_CHAIN_ASM=0, A/B runs)
+  int chain_asm;
 };
 
 // Multi-GPU owner of tile column j (its panel and all its updates): "snake" order over the ranks
@@ -1267,6 +1270,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
 
 }  // namespace tqr
 #include "chain32.hpp"
+#include "chain_asm.hpp"
 #include "xfer.hpp"
 namespace tqr {
 
@@ -1316,7 +1320,14 @@ __global__ __launch_bounds__(C::NT, C::WPC) void k_flow(FlowArgs a) {
     }
 #endif
     if (type == T_CHAIN) {
-      if constexpr (sizeof(S) == 8)
+      if constexpr (sizeof(S) == 8 && C::NW == 8 && (B == 128 || B == 256)) {
+        if (a.chain_asm)
+          flow_chain_asm<B, C>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
+                               s_flag);
+        else
+          flow_chain<B, S, C>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
+                              s_flag);
+      } else if constexpr (sizeof(S) == 8)
         flow_chain<B, S, C>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                          s_flag);
       else

@@ -6,8 +6,9 @@
  *
  *   taskQRP_threads (qrdecomp.c:145): copies matData into matResult and factorises it in
  *     place with tile size b; tau receives the m x n tau matrix (ldm), other entries left
- *     untouched as in the reference. Runs on the GPU; where the reference prints "CPU: x ms"
- *     this prints "GPU (taskQRP_threads, ...): x ms" for the whole call. useWY is accepted; both
+ *     untouched as in the reference. Runs on the GPU; it prints the reference's "CPU: x ms" line
+ *     (same prefix, for scripts that parse it) with "(taskQRP_threads on the GPU, host pointers,
+ *     end to end)" appended, timing the whole call. useWY is accepted; both
  *     values compute the same factorisation (the reference's non-WY kernels are dead code,
  *     SURVEY §2 #7).
  *   SGEQRF / SLARFT / STSQRF / SSSRFT (qrdecomp.c:532, 559, 689, 723): one tile task on the
