@@ -908,8 +908,24 @@ int tqr_plan_create_engine(tqr_plan** out, int m, int n, int b, int dtype, int e
   if (engine != TQR_ENGINE_DEFAULT && engine != TQR_ENGINE_WAVES && engine != TQR_ENGINE_FLOW) return TQR_EINVAL;
   return plan_create(out, m, n, b, dtype, 0, 1, engine);
 }
+// Multi-GPU plans raise the engine's wait limit (flow.hpp g_flow_wait_limit) for this process:
+// peers' launches may start seconds apart. TQR_PEER_TIMEOUT_S (default 60, at least 5).
+static int raise_wait_limit() {
+  static bool done = false;
+  if (done) return TQR_OK;
+  double sec = 60.0;
+  if (const char* e = getenv("TQR_PEER_TIMEOUT_S")) sec = std::max(5.0, atof(e));
+  const unsigned long long ticks = (unsigned long long)(sec * 1e8);  // s_memrealtime: 100 MHz
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_flow_wait_limit), &ticks, sizeof(ticks)));
+  done = true;
+  return TQR_OK;
+}
 int tqr_dist_plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world) {
   if (world < 1 || rank < 0 || rank >= world) return TQR_EINVAL;
+  if (world > 1) {
+    const int st = raise_wait_limit();
+    if (st) return st;
+  }
   return plan_create(out, m, n, b, dtype, rank, world, TQR_ENGINE_FLOW);
 }
 static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world, int engine) {
@@ -1037,9 +1053,10 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
       tqr_plan_destroy(pl); return TQR_EHIP;
     }
     if (world > 1) {
-      // member flags (+ Done[world]) in uncached memory (peers' panels set them over xGMI); zeroed
-      // once: their values are launch epochs (flow.hpp FlowArgs)
-      const size_t nrf = sizeof(int) * ((size_t)pl->kmax * pl->p * pl->ng + world);
+      // member flags (+ Done[world] + Probe[world]) in uncached memory (peers' panels set them over
+      // xGMI); zeroed once: their values are launch epochs (flow.hpp FlowArgs), Probe[r] rank r's
+      // setup token (tqr_dist_probe)
+      const size_t nrf = sizeof(int) * ((size_t)pl->kmax * pl->p * pl->ng + 2 * (size_t)world);
       if (hipExtMallocWithFlags((void**)&pl->d_rf, nrf, hipDeviceMallocUncached) != hipSuccess || hipMemset(pl->d_rf, 0, nrf) != hipSuccess ||
           hipMalloc(&pl->d_peers, sizeof(PeerBufs) * world) != hipSuccess ||
           hipMalloc(&pl->d_peer_wk, sizeof(double*) * (size_t)world * pl->kmax) != hipSuccess) {
@@ -1187,6 +1204,59 @@ int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
   }
   pl->imported = true;
   return TQR_OK;
+}
+
+// ---- peer-path probe (setup): the flag path of the persistent launch, exercised once ----------
+// A panel's owner sets the member flags in its peers' Rf with system-scope stores through the
+// IPC-mapped peer pointers, and the chains poll their own Rf with system-scope loads (flow.hpp).
+// A broken path would otherwise show up only as a 60 s wait timeout inside the first factorisation
+// (or never, as a hang, if the stores are silently lost), so the setup runs the same two operations
+// on a probe word per rank: put (every rank stores its token into each peer's Probe[rank]), a host
+// barrier, then check (every rank loads its own Probe[r] of every peer r).
+static int probe_token(int rank) { return 0x7e510000 | (rank + 1); }
+__global__ void k_probe_put(const PeerBufs* peers, long off, int rank, int world, int token) {
+  const int r = threadIdx.x;
+  if (r < world && r != rank)
+    __hip_atomic_store((__attribute__((address_space(1))) int*)(peers[r].Rf + off + rank), token, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void k_probe_get(int* rf, long off, int world, int* out) {
+  const int r = threadIdx.x;
+  if (r < world) out[r] = ld_sys(rf + off + r);
+}
+int tqr_dist_probe(tqr_plan* pl, int phase, unsigned long long* seen) {
+  if (!pl || pl->world < 2 || !pl->imported || pl->world > 64 || (phase != 0 && phase != 1)) return TQR_EINVAL;
+  const long off = (long)pl->kmax * pl->p * pl->ng + pl->world;  // Probe[] after Done[]
+  if (phase == 0) {
+    hipLaunchKernelGGL(k_probe_put, dim3(1), dim3(64), 0, 0, (const PeerBufs*)pl->d_peers, off, pl->rank, pl->world,
+                       probe_token(pl->rank));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    return TQR_OK;
+  }
+  int* d_out = nullptr;
+  HIPCHK(hipMalloc(&d_out, sizeof(int) * 64));
+  hipLaunchKernelGGL(k_probe_get, dim3(1), dim3(64), 0, 0, pl->d_rf, off, pl->world, d_out);
+  int h[64] = {0};
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpy(h, d_out, sizeof(int) * pl->world, hipMemcpyDeviceToHost);
+  (void)hipFree(d_out);
+  if (e != hipSuccess) {
+    fprintf(stderr, "tqr: rank %d: peer probe failed: %s\n", pl->rank, hipGetErrorString(e));
+    return TQR_EHIP;
+  }
+  unsigned long long got = 0;
+  for (int r = 0; r < pl->world; ++r)
+    if (r != pl->rank && h[r] == probe_token(r)) got |= 1ull << r;
+  if (seen) *seen = got;
+  int st = TQR_OK;
+  for (int r = 0; r < pl->world; ++r)
+    if (r != pl->rank && !((got >> r) & 1)) {
+      fprintf(stderr, "tqr: rank %d does not see rank %d's flag stores (probe word 0x%08x, expected 0x%08x): no working "
+              "peer path for the panel flags\n", pl->rank, r, (unsigned)h[r], (unsigned)probe_token(r));
+      st = TQR_EHIP;
+    }
+  return st;
 }
 
 // Kept for the API: since round 4 every execute resets its own (local) counters, and the

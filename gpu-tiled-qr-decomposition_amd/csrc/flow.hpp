@@ -174,10 +174,15 @@ constexpr unsigned long long FLOW_TIMEOUT = 500000000ull;  // 5 s of s_memrealti
 // host staging the input column by column, as slowly as the host goes (a 32 GiB matrix on one host
 // thread takes several seconds); each expiry that finds the count moved restarts the wait.
 // last: the count seen at the previous expiry (0 before the first: device-resident launches keep
-// the 5 s limit). Cold path only.
+// the 5 s limit). Multi-GPU launches: every wait of a rank may depend, directly or through a local
+// counter, on a peer whose launch started later (process start-up, first touch, a slow host), so
+// once a multi-GPU plan exists the limit is g_flow_wait_limit (tqr_dist_plan_create: 60 s,
+// TQR_PEER_TIMEOUT_S) — read only after the first 5 s. Cold path only.
+__device__ unsigned long long g_flow_wait_limit = FLOW_TIMEOUT;
 __device__ __forceinline__ bool timed_out(unsigned long long& t0, int& last, int* err) {
   const unsigned long long now = __builtin_amdgcn_s_memrealtime();
   if (now - t0 <= FLOW_TIMEOUT) return false;
+  if (now - t0 <= __hip_atomic_load(&g_flow_wait_limit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
   const int pr = __hip_atomic_load((__attribute__((address_space(1))) int*)(err + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (pr != last) {
     last = pr;

@@ -83,6 +83,7 @@ def lib():
     L.tqr_dist_export.argtypes = [_P, ctypes.c_char_p, ctypes.c_size_t]
     L.tqr_dist_import.argtypes = [_P, ctypes.c_char_p, ctypes.c_size_t]
     L.tqr_dist_reset.argtypes = [_P, _P]
+    L.tqr_dist_probe.argtypes = [_P, _I, ctypes.POINTER(ctypes.c_ulonglong)]
     L.tqr_plan_status.argtypes = [_P, _P]
     L.tqr_dist_owner.argtypes = [_P, _I]
     L.tqr_dgeqrt_host.argtypes = [_P, _P, _I, _I, _I, _I]
@@ -194,6 +195,25 @@ def tile_owner(j, world):
     return world - 1 - r if blk % 2 else r
 
 
+def peer_probe(L, h, rank, world, barrier):
+    """The setup's peer-path probe (include/tqr.h tqr_dist_probe): every rank stores its token into
+    each peer's probe word, `barrier()` (all ranks), every rank checks it sees each peer's token
+    through the load path the chains poll. Raises TQRError naming the ranks whose stores did not
+    arrive, before any factorisation could wait on them. Returns the bit mask of peers seen."""
+    st = L.tqr_dist_probe(h, 0, None)
+    if st != 0:
+        raise TQRError(f"DistTiledQR: rank {rank}: peer probe (put) failed: {L.tqr_strerror(st).decode()} ({st})")
+    barrier()
+    seen = ctypes.c_ulonglong(0)
+    st = L.tqr_dist_probe(h, 1, ctypes.byref(seen))
+    missing = [r for r in range(world) if r != rank and not (seen.value >> r) & 1]
+    if st != 0 or missing:
+        raise TQRError(f"DistTiledQR: rank {rank} does not see the flag stores of rank(s) {missing}: "
+                       "no working peer path (xGMI / IPC mapping) for the panel flags; "
+                       "the factorisation would wait on them and time out")
+    return seen.value
+
+
 def owned_tile_cols(q, rank, world):
     """The tile columns 0..q-1 that `rank` owns."""
     return [j for j in range(q) if tile_owner(j, world) == rank]
@@ -245,6 +265,8 @@ class DistTiledQR(TiledQR):
             dist.all_gather_object(every, mine, group=group)
             if any(o != mine for o in every):
                 raise TQRError("DistTiledQR: ranks disagree on the tile-column partition (TQR_DIST_PART)")
+            say("probe")
+            peer_probe(lib(), self.h, self.rank, self.world, lambda: dist.barrier(group=group))
             say("ready")
 
     def owner(self, tile_col):

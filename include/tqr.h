@@ -134,6 +134,13 @@ int tqr_dist_plan_create(tqr_plan** plan, int m, int n, int b, int dtype, int ra
 size_t tqr_dist_handle_bytes(const tqr_plan* plan);
 int tqr_dist_export(tqr_plan* plan, void* handles, size_t len);
 int tqr_dist_import(tqr_plan* plan, const void* all_handles, size_t len);
+/* Peer-path probe, once after tqr_dist_import (fails fast instead of a wait timeout or a hang in the
+ * first factorisation): phase 0 stores this rank's token into every peer's probe word (system-scope
+ * stores through the IPC-mapped peer flags, the path panel flags take); then a host barrier over all
+ * ranks; phase 1 loads this rank's probe words (system-scope loads, the path the chains poll) and
+ * returns TQR_OK if every peer's token arrived, else TQR_EHIP with each missing rank printed.
+ * *seen (may be NULL; phase 1) receives the bit mask of the peers whose token arrived. */
+int tqr_dist_probe(tqr_plan* plan, int phase, unsigned long long* seen);
 /* no-op since round 4 (executes reset their own counters); kept for source compatibility */
 int tqr_dist_reset(tqr_plan* plan, void* stream);
 int tqr_dist_owner(const tqr_plan* plan, int tile_col);

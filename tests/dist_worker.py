@@ -87,6 +87,13 @@ def main():
         A.copy_(L0)
         As.append(A)
         tau_list.append(tau)
+    # test hook: the last rank starts its launches TQR_TEST_SKEW_S seconds after the others (the
+    # others' waits on its flags must outlast the skew: flow.hpp g_flow_wait_limit)
+    skew = float(os.environ.get("TQR_TEST_SKEW_S", "0"))
+    if skew > 0 and rank == world - 1:
+        import time
+        say(f"sleeping {skew} s before the first launch")
+        time.sleep(skew)
     for rep in range(2):
         say(f"run {rep}: execute")
         plan.execute(As[rep], tau_list[rep])

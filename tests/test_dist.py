@@ -125,6 +125,57 @@ def test_ranks_on_one_gpu_match_single_gpu(m, n, b, dt, ranks, mode, extra):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
+def test_rank_launching_late_is_waited_for():
+    """One rank starts its factorisations 8 s after its peer (longer than the single-GPU 5 s wait
+    limit): the peer's waits on its flags outlast the skew (multi-GPU limit 60 s) and both launches
+    still match one GPU bit for bit."""
+    env = dict(os.environ, TQR_FLOW_GRID="96", TQR_TEST_SKEW_S="8")
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.join(HERE, "dist_worker.py"), "1024", "1024", "128", "f64", "0", "gather"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    for run in ("run0", "run1"):
+        assert res[run]["exact"], res[run]
+
+
+class _ProbeLib:
+    """tqr_dist_probe stand-in: phase 1 reports the peers in `seen` (bit mask) and fails if any is
+    missing, as the library does."""
+
+    def __init__(self, world, seen):
+        self.world, self.seen, self.calls = world, seen, []
+
+    def tqr_dist_probe(self, h, phase, out):
+        self.calls.append(phase)
+        if phase == 1:
+            out._obj.value = self.seen
+            return 0 if self.seen == ((1 << self.world) - 1) & ~1 else -3
+        return 0
+
+    def tqr_strerror(self, st):
+        return b"HIP runtime call failed"
+
+
+def test_peer_probe_reports_missing_ranks():
+    """CPU mock of the setup probe: rank 0 of 4 sees ranks 1 and 3 but not 2 -> the error names
+    rank 2 and says why, after put, barrier, check in that order."""
+    L = _ProbeLib(4, 0b1010)
+    order = []
+    with pytest.raises(tqr.TQRError, match=r"rank 0 does not see the flag stores of rank\(s\) \[2\]"):
+        tqr.peer_probe(L, None, 0, 4, lambda: order.append("barrier"))
+    assert L.calls == [0, 1] and order == ["barrier"]
+
+
+def test_peer_probe_passes_when_every_peer_is_seen():
+    L = _ProbeLib(4, 0b1110)
+    assert tqr.peer_probe(L, None, 0, 4, lambda: None) == 0b1110
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
 def test_ranks_with_different_task_lists_fail_at_import():
     """A rank whose task list differs (here its chain segment length) would deadlock the launch:
     tqr_dist_import compares the ranks' list signatures and both ranks fail cleanly instead."""
