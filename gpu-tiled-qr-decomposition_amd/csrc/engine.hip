@@ -772,6 +772,7 @@ struct tqr_plan {
   Item* d_flow = nullptr;
   int nflow = 0;
   int nflow_global = 0;  // tasks of the global list (before a multi-GPU partition)
+  unsigned list_hash = 0;  // FNV-1a of the global list's items in order (plan_signature)
   int* d_sync = nullptr;   // next, err, Rc, Tc, Ac, Rt, Rr
   size_t sync_ints = 0;
   int ns = 1, ng = 1, grid = 256, est_order = 0;
@@ -1020,6 +1021,14 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (const char* eca = getenv("TQR_CHAIN_ASM")) pl->chain_asm = atoi(eca) != 0;
     build_flow_plan(pl->p, pl->q, pl->ns, pl->ng, pl->knobs, fp);
     pl->nflow_global = (int)fp.items.size();
+    {  // FNV-1a of the global list in order: every knob that shapes it (segments, lookahead keys,
+       // TQR_LA / LAC / TG / LAZY) must agree across the ranks (tqr_dist_import)
+      unsigned h = 2166136261u;
+      for (const Item& it : fp.items)
+        for (int v : {it.ts, it.l, it.m, it.k})
+          for (int byte = 0; byte < 4; ++byte) h = (h ^ ((unsigned)v >> (8 * byte) & 0xffu)) * 16777619u;
+      pl->list_hash = h;
+    }
     if (world > 1) partition_flow_plan(fp, rank, world);
     pl->nflow = (int)fp.items.size();
     pl->est_order = fp.est_order;
@@ -1090,10 +1099,10 @@ int tqr_plan_status(tqr_plan* pl, void* stream) {
 static constexpr size_t kBusIdBytes = 64;
 // a rank's handle: PCI bus id, the task-list signature (every rank must partition the same global
 // list: segment lengths, lookahead tail, list length), the IPC handles of Rf and the workspaces
-constexpr size_t kSigInts = 6;
+constexpr size_t kSigInts = 7;
 static void plan_signature(const tqr_plan* pl, int* sig) {
   sig[0] = pl->knobs.seglen; sig[1] = pl->knobs.seglen_la; sig[2] = pl->knobs.la_tail; sig[3] = pl->nflow_global;
-  sig[4] = pl->knobs.tail; sig[5] = pl->knobs.tail_sl;
+  sig[4] = pl->knobs.tail; sig[5] = pl->knobs.tail_sl; sig[6] = (int)pl->list_hash;
 }
 size_t tqr_dist_handle_bytes(const tqr_plan* pl) {
   return pl ? kBusIdBytes + sizeof(int) * kSigInts + sizeof(hipIpcMemHandle_t) * (1 + (size_t)pl->kmax) : 0;
@@ -1170,10 +1179,10 @@ int tqr_dist_import(tqr_plan* pl, const void* all, size_t len) {
     plan_signature(pl, mine);
     if (memcmp(sig, mine, sizeof(sig)) != 0) {  // a launch over different lists would deadlock
       fprintf(stderr, "tqr: rank %d and rank %d built different task lists (segment lengths %d/%d vs %d/%d, "
-              "lookahead tail %d vs %d, tail %d/%d vs %d/%d, %d vs %d tasks): set TQR_SEGLEN / TQR_TAIL / "
-              "TQR_FLOW_GRID alike on every rank\n",
+              "lookahead tail %d vs %d, tail %d/%d vs %d/%d, %d vs %d tasks, list hash %08x vs %08x): set "
+              "TQR_SEGLEN / TQR_TAIL / TQR_LA / TQR_LAC / TQR_TG / TQR_LAZY / TQR_FLOW_GRID alike on every rank\n",
               pl->rank, r, mine[0], mine[1], sig[0], sig[1], mine[2], sig[2], mine[4], mine[5], sig[4], sig[5],
-              mine[3], sig[3]);
+              mine[3], sig[3], (unsigned)mine[6], (unsigned)sig[6]);
       close_opened(pl);
       return TQR_EINVAL;
     }

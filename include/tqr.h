@@ -124,7 +124,8 @@ long tqr_total_tasks(int m, int n, int b);
  * Chain tasks are shorter on 4+ ranks that each launch over a whole device (2 elements instead of
  * 8; TQR_SEGLEN overrides): more parallel slack per rank. Every rank must build the
  * same global task list — tqr_dist_import compares the ranks' list signatures (segment lengths,
- * lookahead tail, tail segments, list length) and fails with TQR_EINVAL if they differ.
+ * lookahead tail, tail segments, list length and a hash of the whole list in order, so every
+ * ordering knob is covered) and fails with TQR_EINVAL if they differ.
  * Setup once: tqr_dist_export -> exchange all ranks' handle blocks (e.g. an all-gather over
  * torch.distributed / MPI) -> tqr_dist_import(plan, blocks of rank 0..world-1). */
 int tqr_dist_plan_create(tqr_plan** plan, int m, int n, int b, int dtype, int rank, int world);

@@ -129,7 +129,7 @@ def test_check_owned_columns_packed_storage(world):
 
 def test_chain_segment_length_rule(monkeypatch):
     """bench.seglen_of mirrors engine.hip env_seglen: 8 on one or two ranks, 2 from four ranks on
-    (tools/sched_sim_seglen.py), TQR_SEGLEN overrides."""
+    (tools/sched_sim.py seglen), TQR_SEGLEN overrides."""
     monkeypatch.delenv("TQR_SEGLEN", raising=False)
     assert [bench.seglen_of(w) for w in (1, 2, 4, 8)] == [8, 8, 2, 2]
     assert bench.seglen_of(4, full=False) == 8  # one-GPU rehearsal: a share of the CUs per rank

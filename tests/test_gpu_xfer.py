@@ -92,7 +92,9 @@ def test_cache_clear_then_reuse(tqr, oracle):
 def test_slow_host_staging_beyond_the_kernel_wait_limit(tqr, oracle):
     """A host that stages the input slower than the engine's 5 s wait limit (one host
     thread on a 32 GiB matrix): every tile column is staged 800 ms late (TQR_HOST_STAGE_DELAY_MS,
-    8 columns: 6.4 s), and the launch's waits on the host use its own, size-scaled limit."""
+    8 columns: 6.4 s). A wait that expires re-arms whenever the launch's upload count has moved
+    since its previous expiry (flow.hpp timed_out: progress-based), so the launch waits for as
+    long as the host keeps staging and completes."""
     m, n, b = 512, 2048, 256
     A = oracle.randzo(m, n, np.float64, seed=9)
     F_ref, T_ref = oracle.factor(A, b)

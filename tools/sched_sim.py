@@ -563,6 +563,8 @@ def simulate_dist_dyn(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, pa
 
 
 def main_dist(argv):
+    """Multi-GPU model: makespan and S(world) per forwarding mode, fine hand-off, dynamic dispatch and
+    the panel cost at which S(8) >= 6. Args: [M] [N] [world ...]"""
     M = int(argv[0]) if len(argv) > 0 else 256
     N = int(argv[1]) if len(argv) > 1 else 64
     worlds = [int(x) for x in argv[2:]] or [1, 2, 4, 8]
@@ -599,17 +601,136 @@ def main_dist(argv):
         print(f"  panel group cycle {cyc:5.1f} us: t1 {t1a / 1e3:6.1f} ms, t8 {t8 / 1e3:6.1f} ms, S(8) = {t1a / t8:4.2f}")
 
 
+def _panel_scaled(a):
+    """every panel cost (factor, T, images, trailing, I/O) scaled by a"""
+    return dict(P, f=P["f"] * a, bt=P["bt"] * a, t=P["t"] * a, io_in=P["io_in"] * a, io_wb=P["io_wb"] * a,
+                io_img=P["io_img"] * a)
+
+
+def _mn(argv, m=256, n=64):
+    return (int(argv[0]) if len(argv) > 0 else m), (int(argv[1]) if len(argv) > 1 else n)
+
+
+def main_seglen(argv):
+    """Chain segment length (TQR_SEGLEN) in the multi-GPU model: makespan and S(world) per segment
+    length, with a per-segment cost (TQR_SIM_SEG us, default 20: calibrated on one MI355X, 65536x16384
+    at segment length 2 vs 8 = 635.3 vs 607.6 ms, i.e. 27.7 ms for ~356k extra segments on 256
+    workgroups). Args: [M] [N] [seglen ...]"""
+    M, N = _mn(argv)
+    sls = [int(x) for x in argv[2:]] or [8, 4, 3, 2]
+    seg = float(os.environ.get("TQR_SIM_SEG", "20"))
+    prm = dict(P, seg=seg)
+    print(f"per-segment cost {seg} us")
+    for sl in sls:
+        items = export_list(M, N, seglen=sl)
+        t1 = simulate_dist(items, M, N, 1, prm=prm)
+        line = f"seglen {sl}: t1 {t1 / 1e3:6.1f} ms"
+        for w in (2, 4, 8):
+            tw = simulate_dist(items, M, N, w, prm=prm)
+            line += f", t{w} {tw / 1e3:6.1f} (S {t1 / tw:4.2f})"
+        print(line, flush=True)
+
+
+def main_2d(argv):
+    """Chain segments spread over the ranks ((j + segment) % world) instead of following their tile
+    column's owner, every cross-rank strip / head-row hand-over charged a flag hop plus a 256 KiB
+    xGMI copy. Args: [M] [N]"""
+    M, N = _mn(argv)
+    items = export_list(M, N)
+    t1 = simulate_dist(items, M, N, 1)
+    for w in (2, 4, 8):
+        tc = simulate_dist(items, M, N, w)
+        t2 = simulate_dist(items, M, N, w, part="2d")
+        print(f"{w} ranks: column partition {tc / 1e3:6.1f} ms (S {t1 / tc:4.2f}); segments spread {t2 / 1e3:6.1f} ms "
+              f"(S {t1 / t2:4.2f})", flush=True)
+
+
+def main_cp(argv):
+    """Critical path with unbounded workgroups (1 and 8 ranks), base / column-granular member
+    hand-off / a faster panel (x0.3). Args: [M] [N]"""
+    M, N = _mn(argv)
+    items = export_list(M, N)
+    fast = _panel_scaled(0.3)
+    for name, prm, fine in (("base", P, None), ("fine", P, (2.0, 2.0)), ("panel x0.3", fast, None),
+                            ("fine+panel x0.3", fast, (1.0, 1.0))):
+        inf = dict(prm, W=20000)
+        cp8 = simulate_dist(items, M, N, 8, prm=inf, fine=fine)
+        cp1 = simulate_dist(items, M, N, 1, prm=inf, fine=fine)
+        print(f"{name:18s}: critical path (unbounded workgroups) 1 rank {cp1 / 1e3:6.1f} ms, 8 ranks {cp8 / 1e3:6.1f} ms",
+              flush=True)
+
+
+def main_fastpanel(argv):
+    """A faster panel (every panel cost scaled by a) under the engine's in-order per-rank dequeue and
+    under dependency-triggered dispatch (simulate_dist_dyn), 1 and 8 ranks. Args: [M] [N] [a ...]"""
+    M, N = _mn(argv)
+    scales = [float(x) for x in argv[2:]] or [1.0, 0.5, 0.3]
+    items = export_list(M, N)
+    for a in scales:
+        pp = _panel_scaled(a)
+        t1 = simulate_dist(items, M, N, 1, prm=pp)
+        t8 = simulate_dist(items, M, N, 8, prm=pp)
+        d1 = simulate_dist_dyn(items, M, N, 1, prm=pp)
+        d8 = simulate_dist_dyn(items, M, N, 8, prm=pp)
+        print(f"panel x{a:.2f}: in-order t1 {t1 / 1e3:6.1f} t8 {t8 / 1e3:6.1f} S {t1 / t8:4.2f} | dynamic t1 {d1 / 1e3:6.1f} "
+              f"t8 {d8 / 1e3:6.1f} S {d1 / d8:4.2f}", flush=True)
+
+
+def main_waits(argv):
+    """Where the workgroups wait under dependency-triggered dispatch, 1 and 8 ranks. Args: [M] [N]"""
+    M, N = _mn(argv)
+    items = export_list(M, N)
+    for w in (1, 8):
+        wt = {}
+        t = simulate_dist_dyn(items, M, N, w, waits=wt)
+        print(f"world {w}: {t / 1e3:.1f} ms")
+        for c in sorted(wt):
+            print(f"   {c:28s} {wt[c] / (w * 256) / 1e3:7.2f} ms/WG")
+
+
+def main_xcd(argv):
+    """ONE GPU, XCD affinity: the tasks of tile column j dequeued only by the 32 workgroups of XCD x(j)
+    (the multi-GPU partition with 8 "ranks" of 32 workgroups, no forwarding), so strips and head rows
+    could be stored write-back into that XCD's L2 (element hand-over e_ld / e_st scaled by h).
+    Args: [M] [N] [h ...]"""
+    M, N = _mn(argv, 64, 64)
+    hs = [float(x) for x in argv[2:]] or [1.0, 0.5, 0.25]
+    items = export_list(M, N)
+    base = simulate_dist(items, M, N, 1)
+    print(f"{M}x{N} tiles: one queue, 256 workgroups: {base / 1e3:.1f} ms")
+    for h in hs:
+        prm = dict(P, W=32, e_ld=P["e_ld"] * h, e_st=P["e_st"] * h)
+        t = simulate_dist(items, M, N, 8, prm=prm, fwd_peer=0.0, hop=0.0)
+        prm1 = dict(P, e_ld=P["e_ld"] * h, e_st=P["e_st"] * h)
+        t1 = simulate_dist(items, M, N, 1, prm=prm1)
+        print(f"  element hand-over x{h:.2f}: per-XCD queues {t / 1e3:.1f} ms; one queue with that hand-over "
+              f"{t1 / 1e3:.1f} ms", flush=True)
+
+
+def main_one(argv):
+    """One GPU, the current order: makespan, per-workgroup waits, and with free panel compute.
+    Args: [M] (square, tiles)"""
+    M = int(argv[0]) if len(argv) > 0 else 64
+    items = export_list(M, M)
+    w = {}
+    span, s, e = simulate(items, M, M, waits=w)
+    print(f"current order: {len(items)} tasks, simulated makespan {span / 1e3:.1f} ms")
+    for c in sorted(w):
+        print(f"  {c:28s} {w[c] / P['W'] / 1e3:7.2f} ms/WG")
+    p0 = dict(P, f=0.0, bt=0.0, t=0.0)
+    span0, _, _ = simulate(items, M, M, prm=p0)
+    print(f"  with free panel compute (PANEL0): {span0 / 1e3:.1f} ms")
+
+
+COMMANDS = {"one": main_one, "dist": main_dist, "seglen": main_seglen, "2d": main_2d, "cp": main_cp,
+            "fastpanel": main_fastpanel, "waits": main_waits, "xcd": main_xcd}
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "dist":
-        main_dist(sys.argv[2:])
+    # python tools/sched_sim.py <command> [args]; a bare number (or nothing) is "one"
+    if len(sys.argv) > 1 and sys.argv[1] in COMMANDS:
+        COMMANDS[sys.argv[1]](sys.argv[2:])
+    elif len(sys.argv) > 1 and sys.argv[1] in ("-h", "--help"):
+        for k, f in COMMANDS.items():
+            print(f"{k:10s} {(f.__doc__ or '').strip().splitlines()[0]}")
     else:
-        M = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-        items = export_list(M, M)
-        w = {}
-        span, s, e = simulate(items, M, M, waits=w)
-        print(f"current order: {len(items)} tasks, simulated makespan {span / 1e3:.1f} ms")
-        for c in sorted(w):
-            print(f"  {c:28s} {w[c] / P['W'] / 1e3:7.2f} ms/WG")
-        p0 = dict(P, f=0.0, bt=0.0, t=0.0)
-        span0, _, _ = simulate(items, M, M, prm=p0)
-        print(f"  with free panel compute (PANEL0): {span0 / 1e3:.1f} ms")
+        main_one(sys.argv[1:])

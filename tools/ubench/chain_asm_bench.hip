@@ -35,7 +35,10 @@ using namespace tqr;
     }                                                                                  \
   } while (0)
 
-constexpr int B = 256;
+#ifndef CAB_B
+#define CAB_B 256
+#endif
+constexpr int B = CAB_B;  // tile size (build with -DCAB_B=128 for 128-row tiles)
 static long LDM = 16384;  // leading dimension of the streamed matrix (argv[3])
 constexpr int NTILE = 64;
 using C = ShapeW8;
