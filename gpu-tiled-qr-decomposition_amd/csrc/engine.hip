@@ -324,26 +324,44 @@ struct ShapeInfo {
   int nw, nt, sw, ib, wpc;
 };
 static ShapeInfo shape_info(int shape) {
-  return shape == 4 ? ShapeInfo{ShapeW4::NW, ShapeW4::NT, ShapeW4::SW, ShapeW4::IB, ShapeW4::WPC}
-                    : ShapeInfo{ShapeW8::NW, ShapeW8::NT, ShapeW8::SW, ShapeW8::IB, ShapeW8::WPC};
+  return shape == 4   ? ShapeInfo{ShapeW4::NW, ShapeW4::NT, ShapeW4::SW, ShapeW4::IB, ShapeW4::WPC}
+         : shape == 5 ? ShapeInfo{ShapeR::NW, ShapeR::NT, ShapeR::SW, ShapeR::IB, ShapeR::WPC}
+                      : ShapeInfo{ShapeW8::NW, ShapeW8::NT, ShapeW8::SW, ShapeW8::IB, ShapeW8::WPC};
 }
 // fp64 default: ShapeW8 — ShapeW4 measured 138.6-139.0 vs 126.7-126.9 ms at 16384^2 (two alternating
 // A/B rounds on one box, profiles/r04/shape_ab); TQR_FLOW_SHAPE=w4 selects it
-static int flow_shape(int dtype) {
+// 5 = ShapeR (chain_res.hpp: one 4-wave workgroup per CU, one wave per SIMD with the whole register
+// file, 64-column strips double-buffered in AGPRs, the head strip resident; fp64, b = 256;
+// TQR_FLOW_SHAPE=r)
+static int flow_shape(int dtype, int b) {
   if (dtype != TQR_F64) return 8;
   const char* e = getenv("TQR_FLOW_SHAPE");
-  return e && strcmp(e, "w4") == 0 ? 4 : 8;
+  if (e && strcmp(e, "w4") == 0) return 4;
+  if (e && strcmp(e, "r") == 0 && b == 256) return 5;
+  return 8;
 }
 static int shape_ib(int shape, int b) { return std::min(b, shape_info(shape).ib); }
 static int shape_ns(int shape, int b) { const int sw = shape_info(shape).sw; return (b + sw - 1) / sw; }
 template <int B, typename S, class C>
 static ffn get_flow() { return k_flow<B, S, C>; }
+template <int B>
+static ffn get_flow_res() {
+  if constexpr (B == 256) return k_flow<256, double, ShapeR>;
+  else return nullptr;
+}
+template <int B>
+static int lds_res() {
+  if constexpr (B == 256) return flow_lds_doubles<256, double, ShapeR>();
+  else return 0;
+}
 static size_t lds_flow(int b, int dtype, int shape) {
   int d = 0;
 #define TQR_L(BB)                                                                                  \
   case BB:                                                                                         \
     d = dtype != TQR_F64 ? flow_lds_doubles<BB, float, ShapeW8>()                                  \
-                         : shape == 4 ? flow_lds_doubles<BB, double, ShapeW4>() : flow_lds_doubles<BB, double, ShapeW8>(); \
+        : shape == 4     ? flow_lds_doubles<BB, double, ShapeW4>()                                 \
+        : shape == 5     ? lds_res<BB>()                                                           \
+                         : flow_lds_doubles<BB, double, ShapeW8>();                                \
     break;
   switch (b) { TQR_L(16) TQR_L(32) TQR_L(64) TQR_L(128) TQR_L(256) }
 #undef TQR_L
@@ -354,7 +372,9 @@ static ffn resolve_flow(int b, int dtype, int shape) {
 #define TQR_F(BB)                                                                                  \
   case BB:                                                                                         \
     f = dtype != TQR_F64 ? get_flow<BB, float, ShapeW8>()                                          \
-                         : shape == 4 ? get_flow<BB, double, ShapeW4>() : get_flow<BB, double, ShapeW8>(); \
+        : shape == 4     ? get_flow<BB, double, ShapeW4>()                                         \
+        : shape == 5     ? get_flow_res<BB>()                                                      \
+                         : get_flow<BB, double, ShapeW8>();                                        \
     break;
   switch (b) { TQR_F(16) TQR_F(32) TQR_F(64) TQR_F(128) TQR_F(256) }
 #undef TQR_F
@@ -766,7 +786,7 @@ struct tqr_plan {
   kfn kp = nullptr, ku = nullptr;
   size_t ldsP = 0, ldsU = 0;
   int profile = 0;
-  int chain_asm = 1;  // fp64 chains on the hand-scheduled MFMA stream (TQR_CHAIN_ASM=0: compiler-scheduled)
+  int chain_asm = 2;  // fp64 chains on the hand-scheduled MFMA stream (TQR_CHAIN_ASM: 0 compiler-scheduled, 1 whole strip loaded in the hand-over, 2 late strip loads)
   // flow engine
   int engine = 1;          // 1 = persistent dataflow (default), 0 = wave-batched launches
   Item* d_flow = nullptr;
@@ -1003,7 +1023,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     tqr_plan_destroy(pl); return TQR_EHIP;
   }
   // persistent dataflow engine: task list, progress counters, panel workspaces, kernel
-  pl->shape = flow_shape(dtype);
+  pl->shape = flow_shape(dtype, b);
   pl->nt = shape_info(pl->shape).nt;
   pl->ns = shape_ns(pl->shape, b);  // chain strips per tile
   pl->ng = b / shape_ib(pl->shape, b);  // reflector groups per tile
@@ -1018,7 +1038,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (const char* gs = getenv("TQR_FLOW_GRID")) pl->grid = std::max(1, atoi(gs));
     FlowPlan fp;
     pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid), default_tail(pl->p, pl->q, dtype), default_la(dtype));
-    if (const char* eca = getenv("TQR_CHAIN_ASM")) pl->chain_asm = atoi(eca) != 0;
+    if (const char* eca = getenv("TQR_CHAIN_ASM")) pl->chain_asm = atoi(eca);  // 0 off, 1 on, 2 late strip loads
     build_flow_plan(pl->p, pl->q, pl->ns, pl->ng, pl->knobs, fp);
     pl->nflow_global = (int)fp.items.size();
     {  // FNV-1a of the global list in order: every knob that shapes it (segments, lookahead keys,
@@ -1301,7 +1321,7 @@ int tqr_dist_owner(const tqr_plan* pl, int tile_col) {
 
 // Host-only task-list helpers below describe the fp64 engine's list (flow_shape(TQR_F64)).
 static void host_flow_plan(int M, int N, int b, int seglen, FlowPlan& fp, const XferPlan* xp = nullptr) {
-  const int sh = flow_shape(TQR_F64);
+  const int sh = flow_shape(TQR_F64, b);
   build_flow_plan(M, N, shape_ns(sh, b), b / shape_ib(sh, b), knobs_from_env(seglen, default_tail(M, N, TQR_F64)), fp, xp);
 }
 int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd) {
@@ -1319,13 +1339,13 @@ int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, in
   return TQR_OK;
 }
 
-int tqr_flow_strip_width(void) { return shape_info(flow_shape(TQR_F64)).sw; }
+int tqr_flow_strip_width(void) { return shape_info(flow_shape(TQR_F64, 256)).sw; }
 
 int tqr_flow_order_check(int M, int N, int b, const int* items, int n) {
   if (M <= 0 || N <= 0 || !valid_b(b) || !items || n <= 0) return TQR_EINVAL;
   std::vector<Item> L(n);
   for (int x = 0; x < n; ++x) L[x] = Item{items[4 * x], items[4 * x + 1], items[4 * x + 2], items[4 * x + 3]};
-  return flow_list_topological(L, M, N, shape_ns(flow_shape(TQR_F64), b)) ? 1 : 0;
+  return flow_list_topological(L, M, N, shape_ns(flow_shape(TQR_F64, b), b)) ? 1 : 0;
 }
 
 int tqr_plan_set_tasks(tqr_plan* pl, const int* items, int n) {

@@ -1276,6 +1276,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
 }  // namespace tqr
 #include "chain32.hpp"
 #include "chain_asm.hpp"
+#include "chain_res.hpp"
 #include "xfer.hpp"
 namespace tqr {
 
@@ -1325,7 +1326,9 @@ __global__ __launch_bounds__(C::NT, C::WPC) void k_flow(FlowArgs a) {
     }
 #endif
     if (type == T_CHAIN) {
-      if constexpr (sizeof(S) == 8 && C::NW == 8 && (B == 128 || B == 256)) {
+      if constexpr (sizeof(S) == 8 && C::NW == 4 && C::WPC == 1 && C::IB == 32 && B == 256) {
+        flow_chain_res<C>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds, s_flag);
+      } else if constexpr (sizeof(S) == 8 && C::NW == 8 && (B == 128 || B == 256)) {
         if (a.chain_asm)
           flow_chain_asm<B, C>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                                s_flag);

@@ -23,9 +23,9 @@ for rep in range(2):
 gridv = ctypes.c_int()
 L.tqr_plan_info(p.h, None, None, None, ctypes.byref(gridv))
 nb = gridv.value  # workgroups of the launch (ShapeW4: two per CU)
-w4 = dt == torch.float64 and os.environ.get("TQR_FLOW_SHAPE") == "w4"
-NW = 4 if w4 else 8  # waves per workgroup
-IB = 16 if w4 else 32  # reflectors per group
+shape = os.environ.get("TQR_FLOW_SHAPE", "w8") if dt == torch.float64 else "w8"
+NW = 4 if shape in ("w4", "r") else 8  # waves per workgroup (r: the resident form, b = 256)
+IB = 16 if shape == "w4" else 32  # reflectors per group
 NC = 24
 st = (ctypes.c_ulonglong * (NC * nb))()
 assert L.tqr_debug_flow_stamps(st, nb) == 0

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(512, 1) void k_group(const double* img, double* X, 
     o.goff = 0;
     o.hsc = (int)sreg(1u);
     if constexpr (MODE == 0) {
-      ca_group<B, false>(o);
+      ca_group<B, 0>(o);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // the updated strip
       if constexpr (B == 256)
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(512, 1) void k_group(const double* img, double* X, 
       o.xout = uniform_rsrc(Xo + colo);
       o.xin = uniform_rsrc(Xn + colo);
       o.hnx = head_rsrc(H + colo, true);
-      ca_group<B, true>(o);
+      ca_group<B, 1>(o);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // the next strip and head rows as loaded by the hand-over: stored behind the updated ones
       if constexpr (B == 256)
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(512, 1) void k_elem(const double* img, double* X, d
       o.goff = __builtin_amdgcn_readfirstlane(g * 256);
       o.hsc = (int)sreg(1u);
       if (g + 1 < ngu || (var & 2)) {
-        ca_group<B, false>(o);
+        ca_group<B, 0>(o);
         if (g + 1 == ngu) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if constexpr (B == 256)
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(512, 1) void k_elem(const double* img, double* X, d
         o.xout = uniform_rsrc(Xo + colo);
         o.xin = null_rsrc(X);
         o.hnx = null_rsrc(X);
-        ca_group<B, true>(o);
+        ca_group<B, 1>(o);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
