@@ -301,3 +301,24 @@ def test_task_order_and_lookahead_segments_bitexact(tqr):
                     os.environ[k] = v
         A3, t3 = run(p3)
         assert torch.equal(A0, A3) and torch.equal(t0, t3), env
+
+
+@pytest.mark.parametrize("env", [{"TQR_CHAIN_ASM": "1"}, {"TQR_CHAIN_ASM": "0"}, {"TQR_FLOW_SHAPE": "r"}])
+@pytest.mark.parametrize("m,n", [(1024, 1024), (2048, 512), (1536, 1280)])
+def test_fp64_chain_forms_vs_oracle(tqr, oracle, monkeypatch, env, m, n):
+    """The fp64 chain forms other than the default (late strip loads in the 8-wave asm chain):
+    the whole strip loaded inside the hand-over (TQR_CHAIN_ASM=1), the compiler-scheduled chain
+    (TQR_CHAIN_ASM=0) and the resident one-wave-per-SIMD form (TQR_FLOW_SHAPE=r, chain_res.hpp)
+    against the oracle at b = 256 (the knobs are read at plan creation: plans cached before are
+    dropped first)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    tqr.cache_clear()
+    try:
+        A = oracle.randzo(m, n, np.float64, seed=7)
+        F_ref, T_ref = oracle.factor(A, 256, threads=8)
+        F = A.copy()
+        T = tqr.geqrt_host(F, 256)
+        assert_close(F, T, F_ref, T_ref)
+    finally:
+        tqr.cache_clear()
