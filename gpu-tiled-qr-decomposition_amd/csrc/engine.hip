@@ -1038,7 +1038,9 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (const char* gs = getenv("TQR_FLOW_GRID")) pl->grid = std::max(1, atoi(gs));
     FlowPlan fp;
     pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid), default_tail(pl->p, pl->q, dtype), default_la(dtype));
-    if (const char* eca = getenv("TQR_CHAIN_ASM")) pl->chain_asm = atoi(eca);  // 0 off, 1 on, 2 late strip loads
+    if (const char* eca = getenv("TQR_CHAIN_ASM")) pl->chain_asm = atoi(eca) & 3;  // 0 off, 1 on, 2 late strip loads
+    // (bit 2: UNMQR elements on the full TSMQR bodies instead of the zero-row-skipping ones; A/B only)
+    if (const char* eu = getenv("TQR_UNMQR_SKIP"); eu && atoi(eu) == 0 && pl->chain_asm) pl->chain_asm |= 4;
     build_flow_plan(pl->p, pl->q, pl->ns, pl->ng, pl->knobs, fp);
     pl->nflow_global = (int)fp.items.size();
     {  // FNV-1a of the global list in order: every knob that shapes it (segments, lookahead keys,

@@ -248,7 +248,8 @@ struct FlowArgs {
   // in the snake and the cyclic partition alike), packed in column order.
   int cdiv;
   // fp64 chains of 128- and 256-tiles on the hand-scheduled MFMA stream (chain_asm.hpp); 0: the
-  // compiler-scheduled flow_chain (TQR_CHAIN_ASM=0, A/B runs)
+  // compiler-scheduled flow_chain (TQR_CHAIN_ASM=0, A/B runs); bits 0-1 the mode (1 whole next strip
+  // loaded in the hand-over, 2 late loads), bit 2 UNMQR elements without the zero-row skip
   int chain_asm;
 };
 
@@ -1329,7 +1330,7 @@ __global__ __launch_bounds__(C::NT, C::WPC) void k_flow(FlowArgs a) {
       if constexpr (sizeof(S) == 8 && C::NW == 4 && C::WPC == 1 && C::IB == 32 && B == 256) {
         flow_chain_res<C>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds, s_flag);
       } else if constexpr (sizeof(S) == 8 && C::NW == 8 && (B == 128 || B == 256)) {
-        if (a.chain_asm)
+        if (a.chain_asm & 3)
           flow_chain_asm<B, C>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                                s_flag);
         else

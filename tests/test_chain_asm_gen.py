@@ -53,3 +53,48 @@ def test_statement_registers(B):
                 lo = int(m.group(1) or m.group(3))
                 assert lo >= g.VLO, line
             assert "a[" not in line and not re.search(r"\bs\d+\b", line), line
+
+
+def _ubodies(g, B, late):
+    NG, lead = B // g.IB, g.XLEAD
+    ub = {}
+    for gg in range(1, NG):
+        if gg + 1 < NG:
+            ub[gg] = g.Body(B, False, skip=8 * gg, early_st=range(4 * (gg - 1), 4 * gg))
+        else:
+            ub[gg] = g.Body(B, True, xlead=lead if late else None, skip=8 * gg, early_st=range(4 * (gg - 1), 4 * gg),
+                            early_ld=[p for p in range(4 * gg) if not late or p < lead])
+        ub[gg].build()
+    return ub
+
+
+@pytest.mark.parametrize("B", [128, 256])
+@pytest.mark.parametrize("late", [False, True])
+def test_unmqr_bodies(B, late):
+    """UNMQR element (GE-type V, zero above group g's rows): group g runs k-steps >= 8 g only —
+    (NKS - 8 g) x 8 MFMAs in each phase plus the T-multiplication's 40 — stores the rows group g-1
+    finished, and the chain's waits still cover every operation (strip stored / next strip loaded
+    exactly once per row pair, checked by simulate) with the hand-over's own sync count."""
+    import re
+    g = _gen()
+    NKS = B // 4
+    ub = _ubodies(g, B, late)
+    for gg, b in ub.items():
+        nm = sum(1 for l in b.s.lines if l.startswith("v_mfma"))
+        assert nm == 2 * 8 * (NKS - 8 * gg) + 40
+        for line in b.s.lines:
+            for m in re.finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", line):
+                assert int(m.group(1) or m.group(3)) >= g.VLO, line
+    plain, ho = g.Body(B, False), g.Body(B, True, xlead=g.XLEAD if late else None)
+    plain.build()
+    ho.build()
+    bodies = (plain, ho)
+    if late:
+        xb = g.Body(B, False, xin_from=g.XLEAD)
+        xb.build()
+        bodies = (plain, ho, xb)
+    for n in (1, 2, 4):
+        assert g.simulate(B, bodies, nelem=n, ubodies=ub)
+    # the plain hand-over's sync count would leave the UNMQR hand-over's LDS-DMA in flight: the
+    # engine uses the generated TQR_CHAIN_ASM_UHANDOVER*_SYNC_B* after an UNMQR element
+    assert ub[B // g.IB - 1].sync_after() < ho.sync_after()
