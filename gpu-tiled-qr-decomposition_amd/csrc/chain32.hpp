@@ -144,8 +144,9 @@ struct XPipe32 {
 
 // One reflector group applied to a strip (X) with head accumulator Hg (TS) or none (GE, UNMQR:
 // the strip is the head tile itself). Phase 1 carries the hook (next group's LDS-DMA), phase 2
-// the post hook (element hand-over).
-template <int B, bool TS, typename Hook, typename Post = NoPost32>
+// the post hook (element hand-over). K0 (GE group g: g NMI): V is zero in tiles mt < K0 (the GE
+// group's unit-lower V, explicit zeros above its rows), so both phases start at tile K0.
+template <int B, bool TS, typename Hook, typename Post = NoPost32, int K0 = 0>
 __device__ __forceinline__ void apply32(const float* VR, const float* TPi, f4v (&X)[Geo32<B>::NMT],
                                         f4v (&Hg)[Geo32<B>::NMT], const Hook& hook, const Post& post = Post()) {
   using G32 = Geo32<B>;
@@ -184,13 +185,14 @@ __device__ __forceinline__ void apply32(const float* VR, const float* TPi, f4v (
 #pragma unroll
   for (int mi = 0; mi < NMI; ++mi) Z[mi] = TS ? Hg[mi] : f4v{0.f, 0.f, 0.f, 0.f};
   // phase 1: Z += V^T X, operands of tile mt+1 read under the MFMAs of tile mt
+  static_assert(K0 % 2 == 0 && K0 < NMT && (TS ? K0 == 0 : true), "K0: even, GE only");
   float ac[4 * NMI], an[4 * NMI];
-  ld1(ac, 0);
+  ld1(ac, K0);
 #pragma unroll
-  for (int mt = 0; mt < NMT; ++mt) {
+  for (int mt = K0; mt < NMT; ++mt) {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
-    hook.step(mt);
+    hook.step(mt - K0);
     if (mt + 1 < NMT) ld1(an, mt + 1);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -199,7 +201,7 @@ __device__ __forceinline__ void apply32(const float* VR, const float* TPi, f4v (
 #pragma unroll
     for (int e = 0; e < 4 * NMI; ++e) ac[e] = an[e];
   }
-  for (int m = NMT; m < Hook::STEPS; ++m) hook.step(m);
+  for (int m = NMT - K0; m < Hook::STEPS; ++m) hook.step(m);
   hook.mid();
   // W = -T^T Z (upper-triangular T: tile pairs mi <= wi, wi-major in the image)
   f4v W[NMI];
@@ -222,7 +224,7 @@ __device__ __forceinline__ void apply32(const float* VR, const float* TPi, f4v (
   // phase 2: X += V W, two tiles interleaved (dependent-accumulator latency 40 > issue 32 cycles)
   float c0[4 * NMI], c1[4 * NMI];
 #pragma unroll
-  for (int mt = 0; mt < NMT; mt += 2) {
+  for (int mt = K0; mt < NMT; mt += 2) {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("" ::: "memory");
     ld2(c0, mt);
@@ -237,6 +239,25 @@ __device__ __forceinline__ void apply32(const float* VR, const float* TPi, f4v (
     post.at(mt, X);  // the previous pair, behind this pair's MFMAs
   }
   post.fin(X);
+}
+
+// The UNMQR element's group g: tiles below g NMI skipped (g wave-uniform; one body per group)
+template <int B, typename Hook>
+__device__ __forceinline__ void apply32_ge(int g, const float* VR, const float* TPi, f4v (&Hd)[Geo32<B>::NMT], const Hook& h) {
+  static_assert(Geo<B>::NG <= 8, "apply32_ge: up to 8 groups");
+#ifdef TQR_NO_GE_SKIP32  // (A/B builds: the full GE V, zero tiles included)
+  g = 0;
+#endif
+  switch (g) {
+    case 0: apply32<B, false, Hook, NoPost32, 0>(VR, TPi, Hd, Hd, h); break;
+    case 1: if constexpr (Geo<B>::NG > 1) apply32<B, false, Hook, NoPost32, 1 * Geo32<B>::NMI>(VR, TPi, Hd, Hd, h); break;
+    case 2: if constexpr (Geo<B>::NG > 2) apply32<B, false, Hook, NoPost32, 2 * Geo32<B>::NMI>(VR, TPi, Hd, Hd, h); break;
+    case 3: if constexpr (Geo<B>::NG > 3) apply32<B, false, Hook, NoPost32, 3 * Geo32<B>::NMI>(VR, TPi, Hd, Hd, h); break;
+    case 4: if constexpr (Geo<B>::NG > 4) apply32<B, false, Hook, NoPost32, 4 * Geo32<B>::NMI>(VR, TPi, Hd, Hd, h); break;
+    case 5: if constexpr (Geo<B>::NG > 5) apply32<B, false, Hook, NoPost32, 5 * Geo32<B>::NMI>(VR, TPi, Hd, Hd, h); break;
+    case 6: if constexpr (Geo<B>::NG > 6) apply32<B, false, Hook, NoPost32, 6 * Geo32<B>::NMI>(VR, TPi, Hd, Hd, h); break;
+    default: if constexpr (Geo<B>::NG > 7) apply32<B, false, Hook, NoPost32, 7 * Geo32<B>::NMI>(VR, TPi, Hd, Hd, h); break;
+  }
 }
 
 // Strip / head tile I/O: tile mt of the strip at column col0 + y, rows 16mt + 4x .. + 3.
@@ -461,7 +482,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
             for (int mi = 0; mi < NMI; ++mi) Hd[NMT - NMI + mi] = tmp[mi];
             FST(2);
           } else {
-            apply32<B, false>(VRp, TPi, Hd, Hd, dh);
+            apply32_ge<B>(g, VRp, TPi, Hd, dh);
             FST(13);
           }
         } else {

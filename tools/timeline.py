@@ -58,3 +58,15 @@ for kk in (0, 1, 16):
     order = pm[np.argsort(I[pm, 1])]
     rows = [f"{I[x, 1]}:{s[x] / 1e3:.2f}-{e[x] / 1e3:.2f}" for x in order[:: max(1, len(order) // 12)]]
     print(f" step {kk} members (tile row: start-end ms): " + " ".join(rows))
+# every task of the last N steps in start order (TQR_TIMELINE_TAIL=N): the tail's critical path
+NT = int(os.environ.get("TQR_TIMELINE_TAIL", "0"))
+if NT:
+    print(f" tasks of steps >= {K - NT} (start..end ms, workgroup, task):")
+    sel = np.where(k >= K - NT)[0]
+    for x in sel[np.argsort(s[sel])]:
+        if chain[x]:
+            i0, i1 = I[x, 1] & 0xffff, I[x, 1] >> 16
+            desc = f"CHAIN k={k[x]} j={I[x, 2]} strip={(I[x, 0] >> 8) & 0xff} seg={I[x, 3] >> 16} rows {i0}..{i1 - 1}"
+        else:
+            desc = f"PANEL type={typ[x]} k={k[x]} row={I[x, 1]}"
+        print(f"  {s[x] / 1e3:8.3f}..{e[x] / 1e3:8.3f}  wg {T[x, 2]:3d}  {desc}")
