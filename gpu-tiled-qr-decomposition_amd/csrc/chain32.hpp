@@ -414,7 +414,7 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
           publish_after_drain(pending, 1);
           pending = nullptr;
         }
-        if (!has_next && g > 0) publish_after_drain(&acg[g - 1], 1);
+        if (!has_next && ts && g > 0) publish_after_drain(&acg[g - 1], 1);  // (a lone UNMQR: at the end)
         if (t == FLOW_PT) {  // early load of the counter the next sync point will test
           const int tg = next_test_group<NG>(g);
           const bool here = g + 2 < NG;
@@ -515,6 +515,8 @@ __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, in
   }
   sync_point<true, true>(true, sflag, par);
   if (pending) publish_after_drain(pending, 1);
+  if (seg == 0 && i0 >= i1)  // a segment of the UNMQR element alone: its head strip stored whole above
+    for (int g = 0; g + 1 < NG; ++g) publish_after_drain(&acg[g], 1);
   publish_after_drain(&acg[NG - 1], 1);
   FST(4);
 }

@@ -495,11 +495,13 @@ struct XferPlan {
 //              element instead of behind it
 //   tail       the last `tail` steps (TQR_TAIL; default: default_tail): every chain tail_sl elements
 //              per segment (TQR_TAIL_SEGLEN, default 1)
+//   ualone     the last ualone steps (TQR_UNMQR_ALONE; default: tail): the lookahead column's UNMQR
+//              element alone in segment 0 (flow.hpp unmqr_alone)
 //   Tg         the estimator's panel group-step cost in chain elements (TQR_TG, default 1.4)
 //   lazy       TQR_LAZY (default 1), la / lac: TQR_LA (default: default_la) / TQR_LAC (see
 //              build_flow_plan)
 struct FlowKnobs {
-  int seglen = 8, seglen_la = 8, la_tail = 0, tail = 0, tail_sl = 1;
+  int seglen = 8, seglen_la = 8, la_tail = 0, tail = 0, tail_sl = 1, ualone = 0;
   double Tg = 1.4, lazy = 1.0, la = 0.0, lac = 0.0;
 };
 // Default tail (fp64 storage): the steps whose columns have at most kTailRows rows below the
@@ -532,6 +534,8 @@ static FlowKnobs knobs_from_env(int seglen, int tail_default = 0, double la_defa
   kn.la_tail = e ? std::max(0, atoi(e)) : 0;
   if (const char* et = getenv("TQR_TAIL")) kn.tail = std::max(0, atoi(et));
   if (const char* ets = getenv("TQR_TAIL_SEGLEN")) kn.tail_sl = std::max(1, atoi(ets));
+  kn.ualone = kn.tail;
+  if (const char* eua = getenv("TQR_UNMQR_ALONE")) kn.ualone = std::max(0, atoi(eua));
   if (const char* eg = getenv("TQR_TG")) kn.Tg = atof(eg);
   if (const char* el = getenv("TQR_LAZY")) kn.lazy = atof(el);
   if (const char* ela = getenv("TQR_LA")) kn.la = atof(ela);
@@ -597,6 +601,7 @@ static void build_flow_plan(int p, int q, int ns, int ng, const FlowKnobs& kn, F
       std::vector<double> seg_start;
       seg_start.push_back(t0);
       const int seglen = seglen_of(k, j);
+      const bool ua = unmqr_alone(k, j, kmax, kn.ualone) && p - k - 1 > 0;  // segment 0: the UNMQR alone
       for (int i = k + 1; i < p; ++i) {
         double st = std::max({prev, fin_prev(k, i, j), pstart[(size_t)k * p + i] + Tg});
         if ((i - k - 1) % seglen == 0 && i > k + 1) seg_start.push_back(st);
@@ -604,10 +609,13 @@ static void build_flow_plan(int p, int q, int ns, int ng, const FlowKnobs& kn, F
         fin[id3(k, i, j)] = f;
         prev = f;
       }
-      int nseg = p - k - 1 > 0 ? (p - k - 1 + seglen - 1) / seglen : 1;
+      const int nseg = nseg_of_chain(k, j, p, kmax, seglen, kn.ualone);
+      if (ua) seg_start.insert(seg_start.begin(), t0);
       for (int e = 0; e < nseg; ++e) {
-        int i0 = k + 1 + e * seglen, i1 = std::min(p, i0 + seglen);
+        const int er = ua ? e - 1 : e;  // the segment's run of rows
+        int i0 = k + 1 + er * seglen, i1 = std::min(p, i0 + seglen);
         if (p - k - 1 == 0) { i0 = p; i1 = p; }
+        if (er < 0) i0 = i1 = k + 1;  // (the UNMQR-only segment: no rows)
         // lazy keys (TQR_LAZY, default 1): a segment of a non-lookahead column is keyed by the
         // estimated completion of its first panel member, so a workgroup does not dequeue it
         // long before its V/T images exist (it would wait group by group); the lookahead
@@ -640,8 +648,8 @@ static void build_flow_plan(int p, int q, int ns, int ng, const FlowKnobs& kn, F
       else if (ty == T_UP || ty == T_DOWN) idx[std::make_tuple(ty, it.m, (it.ts >> 8) & 0xff, 0, 0)] = x;
       else idx[std::make_tuple(0, it.l, it.k, 0, 0)] = x;
     }
-    auto seg_of = [&](int k, int j, int i) { return (i - k - 1) / seglen_of(k, j); };
-    auto nseg_of = [&](int k, int j) { return p - k - 1 > 0 ? (p - k - 1 + seglen_of(k, j) - 1) / seglen_of(k, j) : 1; };
+    auto seg_of = [&](int k, int j, int i) { return seg_of_row(k, j, i, kmax, seglen_of(k, j), kn.ualone); };
+    auto nseg_of = [&](int k, int j) { return nseg_of_chain(k, j, p, kmax, seglen_of(k, j), kn.ualone); };
     for (int x = 0; x < (int)tl.size(); ++x) {
       const Item& it = tl[x].it;
       int ty = it.ts & 0xff;
@@ -1041,6 +1049,8 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (const char* eca = getenv("TQR_CHAIN_ASM")) pl->chain_asm = atoi(eca) & 3;  // 0 off, 1 on, 2 late strip loads
     // (bit 2: UNMQR elements on the full TSMQR bodies instead of the zero-row-skipping ones; A/B only)
     if (const char* eu = getenv("TQR_UNMQR_SKIP"); eu && atoi(eu) == 0 && pl->chain_asm) pl->chain_asm |= 4;
+    // (bit 3: fp32 storage on the compiler-scheduled flow_chain32; A/B only)
+    if (const char* e32 = getenv("TQR_CHAIN32_ASM"); e32 && atoi(e32) == 0) pl->chain_asm |= 8;
     build_flow_plan(pl->p, pl->q, pl->ns, pl->ng, pl->knobs, fp);
     pl->nflow_global = (int)fp.items.size();
     {  // FNV-1a of the global list in order: every knob that shapes it (segments, lookahead keys,
@@ -1477,7 +1487,7 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     f.epoch = pl->world > 1 ? pl->epoch + 1 : 0;
     f.chain_asm = pl->chain_asm;
     f.seglen = pl->knobs.seglen; f.seglen_la = pl->knobs.seglen_la; f.la_tail = pl->knobs.la_tail;
-    f.tail = pl->knobs.tail; f.tail_sl = pl->knobs.tail_sl;
+    f.tail = pl->knobs.tail; f.tail_sl = pl->knobs.tail_sl; f.ualone = pl->knobs.ualone;
     if (xa) {
       f.hsrc = xa->hsrc; f.hdst = xa->hdst; f.hld = xa->hld; f.hup = xa->hup; f.hdn = xa->hdn; f.gen = xa->gen;
       f.Uc = f.Rr + (size_t)pl->kmax * pl->ng;

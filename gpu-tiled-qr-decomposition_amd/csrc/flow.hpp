@@ -241,7 +241,7 @@ struct FlowArgs {
   int* hup;
   int* hdn;
   int* Uc;
-  int gen, nxc, xrows, seglen, seglen_la, la_tail, tail, tail_sl;
+  int gen, nxc, xrows, seglen, seglen_la, la_tail, tail, tail_sl, ualone;
   // storage of the tile columns: global tile column j is local column j / cdiv of A (and tau
   // column k of panel k local column k / cdiv). Single GPU: cdiv = 1. Multi-GPU: cdiv = world —
   // a rank stores only the tile columns it owns (one per block of `world` consecutive columns,
@@ -249,7 +249,8 @@ struct FlowArgs {
   int cdiv;
   // fp64 chains of 128- and 256-tiles on the hand-scheduled MFMA stream (chain_asm.hpp); 0: the
   // compiler-scheduled flow_chain (TQR_CHAIN_ASM=0, A/B runs); bits 0-1 the mode (1 whole next strip
-  // loaded in the hand-over, 2 late loads), bit 2 UNMQR elements without the zero-row skip
+  // loaded in the hand-over, 2 late loads), bit 2 UNMQR elements without the zero-row skip, bit 3
+  // fp32 storage on flow_chain32 (else flow_chain32_asm)
   int chain_asm;
 };
 
@@ -274,6 +275,20 @@ __host__ __device__ inline int seglen_of_chain(int k, int j, int kmax, int segle
   if (k >= kmax - tail) return tail_sl;
   if (j != k + 1) return seglen;
   return k >= kmax - la_tail ? 1 : seglen_la;
+}
+// The last `ualone` steps' lookahead column (j = k+1) runs its UNMQR element alone in segment 0:
+// the element that finishes the next diagonal tile, TSMQR(k+1, k+1, k), then starts segment 1,
+// pipelined group by group behind the UNMQR (Ac) instead of running after it in the same task.
+__host__ __device__ inline bool unmqr_alone(int k, int j, int kmax, int ualone) { return j == k + 1 && k >= kmax - ualone; }
+// segments of chain (k, j) with segment length sl: rows k+1 .. p-1 in runs of sl, after the
+// UNMQR-only segment when unmqr_alone; the segment holding row i > k
+__host__ __device__ inline int nseg_of_chain(int k, int j, int p, int kmax, int sl, int ualone) {
+  const int rows = p - k - 1;
+  if (rows <= 0) return 1;
+  return (rows + sl - 1) / sl + (unmqr_alone(k, j, kmax, ualone) ? 1 : 0);
+}
+__host__ __device__ inline int seg_of_row(int k, int j, int i, int kmax, int sl, int ualone) {
+  return (i - k - 1) / sl + (unmqr_alone(k, j, kmax, ualone) ? 1 : 0);
 }
 
 // ---- synchronisation ---------------------------------------------------------------------
@@ -1178,7 +1193,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
         pending = nullptr;
       }
       // segment's last element: its head rows of group g-1 (stored write-through) are drained
-      if (!has_next && g > 0) publish_after_drain(&acg[g - 1], 1);
+      if (!has_next && ts && g > 0) publish_after_drain(&acg[g - 1], 1);  // (a lone UNMQR: at the end)
       if (t == PT) {  // early load of the counter the next sync point will test
         const int tg = next_test_group<NG>(g);
         const bool here = g + 2 < NG;  // this element's counter, else the next element's
@@ -1266,9 +1281,12 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
     pending = tc(i);
     FST(4);
   }
-  // last element's strip and its last head-row group: drain, then publish both
+  // last element's strip and its last head-row group: drain, then publish both (a segment of the
+  // UNMQR element alone: its strip is the head tile, stored whole at its end — every group)
   sync_point<true, false, PT>(true, sflag, par);
   if (pending) publish_after_drain(pending, 1);
+  if (seg == 0 && i0 >= i1)
+    for (int g = 0; g + 1 < NG; ++g) publish_after_drain(&acg[g], 1);
   publish_after_drain(&acg[NG - 1], 1);
   FST(4);
 }
@@ -1277,6 +1295,7 @@ __device__ __noinline__ void flow_chain(const FlowArgs& a, int s_, int i0_, int 
 }  // namespace tqr
 #include "chain32.hpp"
 #include "chain_asm.hpp"
+#include "chain32_asm.hpp"
 #include "chain_res.hpp"
 #include "xfer.hpp"
 namespace tqr {
@@ -1339,7 +1358,14 @@ __global__ __launch_bounds__(C::NT, C::WPC) void k_flow(FlowArgs a) {
       } else if constexpr (sizeof(S) == 8)
         flow_chain<B, S, C>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                          s_flag);
-      else
+      else if constexpr (C::NW == 8 && (B == 128 || B == 256)) {
+        if ((a.chain_asm & 3) && !(a.chain_asm & 8))
+          flow_chain32_asm<B, C>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16,
+                                 lds, s_flag);
+        else
+          flow_chain32<B>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
+                          s_flag);
+      } else
         flow_chain32<B>(a, (it.ts >> 8) & 0xff, it.l & 0xffff, it.l >> 16, it.m, it.k & 0xffff, it.k >> 16, lds,
                         s_flag);
     } else if (type == T_UP || type == T_DOWN) {

@@ -30,7 +30,7 @@ __device__ __noinline__ bool column_final(const FlowArgs& a, int j, int NG) {
   const int kend = min(j, a.kmax);
   for (int i = 0; i < kend; ++i) {
     const int sl = seglen_of_chain(i, j, a.kmax, a.seglen, a.seglen_la, a.la_tail, a.tail, a.tail_sl);
-    const int nseg = a.p - i - 1 > 0 ? (a.p - i - 1 + sl - 1) / sl : 1;
+    const int nseg = nseg_of_chain(i, j, a.p, a.kmax, sl, a.ualone);
     for (int s = 0; s < a.ns; ++s)
       if (!spin_ge(&a.Ac[(((size_t)i * a.q + j) * a.ns + s) * NG + NG - 1], nseg, a.err)) return false;
   }

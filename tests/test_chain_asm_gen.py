@@ -98,3 +98,42 @@ def test_unmqr_bodies(B, late):
     # the plain hand-over's sync count would leave the UNMQR hand-over's LDS-DMA in flight: the
     # engine uses the generated TQR_CHAIN_ASM_UHANDOVER*_SYNC_B* after an UNMQR element
     assert ub[B // g.IB - 1].sync_after() < ho.sync_after()
+
+
+def _gen32():
+    spec = importlib.util.spec_from_file_location("gen_chain32_asm", PKG / "gen" / "gen_chain32_asm.py")
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_chain32_generated_text_is_committed(tmp_path, monkeypatch):
+    """fp32 chain statements (gen_chain32_asm.py): the committed chain32_asm_gen.inc is current."""
+    g = _gen32()
+    out = tmp_path / "chain32_asm_gen.inc"
+    monkeypatch.setattr("sys.argv", ["gen_chain32_asm.py", str(out)])
+    g.main()
+    assert out.read_text() == (PKG / "csrc" / "chain32_asm_gen.inc").read_text()
+
+
+@pytest.mark.parametrize("B", [128, 256])
+def test_chain32_bodies(B):
+    """fp32 bodies: MFMA counts (phase 1 and 2: 8 per tile, T: 12; UNMQR group g skips 2 g tiles),
+    registers within the statements' range, and the counted waits of chains of 1-5 elements with
+    both hand-over forms (simulate: each group's LDS-DMA at its sync point, each strip tile before
+    its first MFMA, every strip stored and loaded exactly once)."""
+    import re
+    g = _gen32()
+    NMT = B // 16
+    plain, ho, hol, xb = g.Body32(B), g.Body32(B, handover=True), g.Body32(B, handover=True, xlead=g.XLEAD), g.Body32(B, xin_from=g.XLEAD)
+    bodies = [plain, ho, hol, xb] + [g.Body32(B, ts=False, k0=2 * u) for u in range(B // 32)]
+    for b in bodies:
+        b.build()
+        nm = sum(1 for l in b.s.lines if l.startswith("v_mfma"))
+        assert nm == 2 * 8 * (NMT - b.k0) + 12
+        for line in b.s.lines:
+            for m in re.finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", line):
+                assert int(m.group(1) or m.group(3)) >= g.VLO, line
+    for n in (1, 2, 3, 5):
+        assert g.simulate(B, plain, ho, None, n)
+        assert g.simulate(B, plain, hol, xb, n)

@@ -92,5 +92,32 @@ def test_flow_plan_topological(tqr, M, N, b, seg):
     tail = max(0, min(kmax, kmax - (M - 1 - 31)))
     sl = lambda k: 1 if k >= kmax - tail else seg
     chains = sum((N - k - 1) * ns * max(1, -(-(M - k - 1) // sl(k))) for k in range(kmax))
+    # ... and their lookahead column's UNMQR element in a segment of its own (flow.hpp unmqr_alone)
+    chains += sum(ns for k in range(kmax) if k >= kmax - tail and M - k - 1 > 0 and k + 1 < N)
     assert n.value == panels + chains
     assert o.value == 1
+
+
+@pytest.mark.parametrize("M,N,b", [(8, 8, 64), (8, 8, 128), (64, 64, 256), (16, 6, 256), (6, 16, 256)])
+def test_flow_plan_segments_below_diagonal(tqr, M, N, b):
+    """Every chain segment's rows lie strictly below its step's diagonal tile and segments of one
+    chain tile its rows exactly once (the lookahead column's UNMQR-only segment has none): the
+    kernel's element loop starts at the UNMQR (segment 0) and runs rows i0 .. i1-1."""
+    import ctypes
+    cap = 4 * 100000
+    buf = (ctypes.c_int * cap)()
+    n = tqr.lib().tqr_flow_plan_export(M, N, b, 8, buf, cap)
+    assert 0 < n <= cap // 4
+    rows = {}
+    for x in range(n):
+        ts, l, m, k = buf[4 * x:4 * x + 4]
+        if ts & 0xff != 4:
+            continue
+        kk, e, i0, i1, s = k & 0xffff, k >> 16, l & 0xffff, l >> 16, (ts >> 8) & 0xff
+        assert kk + 1 <= i0 <= i1 <= M, (kk, m, e, i0, i1)
+        rows.setdefault((kk, m, s), []).append((e, i0, i1))
+    for (kk, j, s), segs in rows.items():
+        segs.sort()
+        assert [e for e, _, _ in segs] == list(range(len(segs)))
+        covered = [i for _, i0, i1 in segs for i in range(i0, i1)]
+        assert covered == list(range(kk + 1, M)), (kk, j, segs)

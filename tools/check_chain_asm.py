@@ -34,7 +34,7 @@ def regs(line):
 
 def check(path):
     lines = open(path).read().split("\n")
-    starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\S*flow_chain_(asm|res)\S*:", l)]
+    starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\S*flow_chain(?:32)?_(asm|res)\S*:", l)]
     if not starts:
         print("check_chain_asm: no flow_chain_asm in", path)
         return 1
