@@ -53,6 +53,8 @@ def test_factor_vs_reference(tqr, oracle, name):
     (2048, 512, 256, np.float64),    # tall-skinny, flat TS chain of 8
     (512, 512, 64, np.float32),
     (1024, 1024, 256, np.float32),
+    (1024, 768, 128, np.float32),    # fp32 asm chain, 128-tiles
+    (4096, 512, 256, np.float32),    # fp32: two chain segments per column (head strip handed on)
 ])
 def test_factor_vs_oracle(tqr, oracle, m, n, b, dt):
     A = oracle.randzo(m, n, dt, seed=5)
@@ -319,6 +321,28 @@ def test_fp64_chain_forms_vs_oracle(tqr, oracle, monkeypatch, env, m, n):
         F_ref, T_ref = oracle.factor(A, 256, threads=8)
         F = A.copy()
         T = tqr.geqrt_host(F, 256)
+        assert_close(F, T, F_ref, T_ref)
+    finally:
+        tqr.cache_clear()
+
+
+@pytest.mark.parametrize("env", [{"TQR_CHAIN_ASM": "1"}, {"TQR_CHAIN32_ASM": "0"}, {"TQR_UNMQR_ALONE": "0"},
+                                 {"TQR_TAIL": "64", "TQR_UNMQR_ALONE": "64"}])
+@pytest.mark.parametrize("m,n,b,dt", [(4096, 768, 256, np.float32), (1024, 1024, 128, np.float32),
+                                      (1536, 1280, 256, np.float64)])
+def test_chain_knobs_vs_oracle(tqr, oracle, monkeypatch, env, m, n, b, dt):
+    """Non-default chain knobs on both precisions: the fp32 asm chain with the whole next strip
+    loaded in the hand-over (TQR_CHAIN_ASM=1) and the compiler-scheduled fp32 chain
+    (TQR_CHAIN32_ASM=0); the tail's lookahead UNMQR-alone segments off (TQR_UNMQR_ALONE=0) and on
+    for every step with one-element segments (also for fp32, whose default tail is 0)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    tqr.cache_clear()
+    try:
+        A = oracle.randzo(m, n, dt, seed=11)
+        F_ref, T_ref = oracle.factor(A, b, threads=8)
+        F = A.copy()
+        T = tqr.geqrt_host(F, b)
         assert_close(F, T, F_ref, T_ref)
     finally:
         tqr.cache_clear()
