@@ -523,7 +523,21 @@ static int default_tail(int p, int q, int dtype) {
 // 467.7; round 4's earlier 4 vs 0: 469.0-469.1 vs 470.4-470.7), 0 for fp64 (2: +0.1-0.2 ms;
 // profiles/r04/la_f32/).
 static double default_la(int dtype) { return dtype == TQR_F32 ? 2.0 : 0.0; }
-static FlowKnobs knobs_from_env(int seglen, int tail_default = 0, double la_default = 0.0) {
+// Multi-rank defaults (4+ ranks, each launch covering its whole device — the plans of the 8-GPU
+// run): besides 2-element segments (env_seglen), one-element segments in the last 7/16 of the steps
+// (28 of 64 at 65536x16384) and the lookahead column's chains keyed 4 elements earlier. The model
+// with round-5 chain costs (tools/sched_sim.py dist5): S(8) 6.41 against 6.16 with
+// 2-element segments alone (tail 24 / 32: 6.35 / 6.39 with the keying, 6.38 at 32 without).
+struct MultiRankDefaults {
+  int tail;
+  double lac;  // < 0: the panel keying (TQR_LA's default)
+};
+static MultiRankDefaults multi_rank_defaults(int p, int q, int dtype, int world, bool full) {
+  const int kmax = std::min(p, q);
+  if (world >= 4 && full) return {std::max(default_tail(p, q, dtype), 7 * kmax / 16), 4.0};
+  return {default_tail(p, q, dtype), -1.0};
+}
+static FlowKnobs knobs_from_env(int seglen, int tail_default = 0, double la_default = 0.0, double lac_default = -1.0) {
   FlowKnobs kn;
   kn.seglen = std::max(1, seglen);
   kn.tail = tail_default;
@@ -539,7 +553,7 @@ static FlowKnobs knobs_from_env(int seglen, int tail_default = 0, double la_defa
   if (const char* eg = getenv("TQR_TG")) kn.Tg = atof(eg);
   if (const char* el = getenv("TQR_LAZY")) kn.lazy = atof(el);
   if (const char* ela = getenv("TQR_LA")) kn.la = atof(ela);
-  kn.lac = kn.la;
+  kn.lac = lac_default >= 0.0 ? lac_default : kn.la;
   if (const char* elac = getenv("TQR_LAC")) kn.lac = atof(elac);  // lookahead column's chains (default: TQR_LA)
   return kn;
 }
@@ -1045,7 +1059,8 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     pl->grid = full_grid;
     if (const char* gs = getenv("TQR_FLOW_GRID")) pl->grid = std::max(1, atoi(gs));
     FlowPlan fp;
-    pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid), default_tail(pl->p, pl->q, dtype), default_la(dtype));
+    const MultiRankDefaults mrd = multi_rank_defaults(pl->p, pl->q, dtype, world, pl->grid >= full_grid);
+    pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid), mrd.tail, default_la(dtype), mrd.lac);
     if (const char* eca = getenv("TQR_CHAIN_ASM")) pl->chain_asm = atoi(eca) & 3;  // 0 off, 1 on, 2 late strip loads
     // (bit 2: UNMQR elements on the full TSMQR bodies instead of the zero-row-skipping ones; A/B only)
     if (const char* eu = getenv("TQR_UNMQR_SKIP"); eu && atoi(eu) == 0 && pl->chain_asm) pl->chain_asm |= 4;

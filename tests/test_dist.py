@@ -105,6 +105,11 @@ def test_partition_gloo_world2():
                                                        (2048, 2048, 256, "f64", 4, "gather", {}),
                                                        # the 8-GPU default segment length (2) against one GPU's (8)
                                                        (2048, 2048, 256, "f64", 4, "gather", {"TQR_SEGLEN": "2", "TQR_TEST_REF_SEGLEN": "8"}),
+                                                       # ... and the rest of the 8-GPU defaults: one-element segments in the last
+                                                       # 7/16 of the steps with the lookahead column keyed 4 elements earlier
+                                                       (2048, 2048, 256, "f64", 4, "gather", {"TQR_SEGLEN": "2", "TQR_TAIL": "3",
+                                                                                              "TQR_TAIL_SEGLEN": "1", "TQR_LAC": "4",
+                                                                                              "TQR_TEST_REF_SEGLEN": "8"}),
                                                        # BASELINE configs[3] shape at full size
                                                        (65536, 16384, 256, "f64", 2, "checksum", {})])
 def test_ranks_on_one_gpu_match_single_gpu(m, n, b, dt, ranks, mode, extra):

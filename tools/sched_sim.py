@@ -276,6 +276,14 @@ def owner_of(j, world, kind="cyclic"):
     return j % world
 
 
+def _cg(prm, unmqr, g, NG):
+    """a chain group's duration: an UNMQR element's group g runs only the rows below the group
+    (round 5: prm["uskip"], phases 1 and 2 from k-step 8 g), at prm["c0"] fixed cost"""
+    if unmqr and prm.get("uskip"):
+        return prm.get("c0", 1.5) + (prm["c"] - prm.get("c0", 1.5)) * (NG - g) / NG
+    return prm["c"]
+
+
 def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="idle", trace=None, pres=0,
                   part="snake", fine=None):
     """The engine on `world` GPUs of W workgroups each: rank r runs the tasks of the global list
@@ -371,7 +379,7 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
                     st = max(t, av[g], need)
                     if pg is not None and idx == 0:
                         st = max(st, pg[min(g + 1, NG - 1)])
-                    t = st + prm["c"]
+                    t = st + _cg(prm, i == k, g, NG)
                     g_t[g] = t
                 t += prm["e_st"]
                 Tc[(i, j, s, k)] = t
@@ -722,7 +730,47 @@ def main_one(argv):
     print(f"  with free panel compute (PANEL0): {span0 / 1e3:.1f} ms")
 
 
-COMMANDS = {"one": main_one, "dist": main_dist, "seglen": main_seglen, "2d": main_2d, "cp": main_cp,
+# round-5 chain costs: the asm chain's group 16.3 us, the element hand-over with
+# late strip loads +6 us in the hand-over group and +5 us in the next element's first group, the
+# UNMQR element skipping the GE V's zero rows
+P5 = dict(P, c=16.3, e_ld=5.0, e_st=6.0, uskip=1, c0=1.5)
+
+
+def main_dist5(argv):
+    """The 8-GPU model with round-5 chain costs (P5): one GPU at the engine's segment length 8, N
+    ranks at its multi-rank default 2, and list / segment variants (environment knobs of the task
+    list, TQR_*, read by the library's plan export). Args: [M] [N] [world]"""
+    M, N = _mn(argv)
+    w = int(argv[2]) if len(argv) > 2 else 8
+    seg = float(os.environ.get("TQR_SIM_SEG", "20"))
+    prm = dict(P5, seg=seg)
+    t1 = simulate_dist(export_list(M, N, seglen=8), M, N, 1, prm=prm)
+    print(f"{M}x{N} tiles, round-5 costs, per-segment {seg} us: t1 {t1 / 1e3:.1f} ms (segment length 8)", flush=True)
+    variants = [("seglen 2 (round 4 default)", {}),
+                ("round-5 8-GPU default", {"TQR_TAIL": str(7 * min(M, N) // 16), "TQR_TAIL_SEGLEN": "1", "TQR_LAC": "4"}),
+                ("seglen_la 1", {"TQR_SEGLEN_LA": "1"}),
+                ("lookahead column keyed 4 earlier", {"TQR_LAC": "4"}), ("panels keyed 2 earlier", {"TQR_LA": "2"}),
+                ("seglen 3", {"TQR_SEGLEN": "3"})]
+    if os.environ.get("TQR_SIM_VARIANTS"):  # "name:K=V,K=V;name:..." replaces the list
+        variants = [(v.split(":")[0], dict(kv.split("=") for kv in v.split(":")[1].split(",") if kv))
+                    for v in os.environ["TQR_SIM_VARIANTS"].split(";")]
+    for name, env in variants:
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            sl = int(os.environ.get("TQR_SEGLEN", "2"))
+            items = export_list(M, N, seglen=sl)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k)
+                else:
+                    os.environ[k] = v
+        tw = simulate_dist(items, M, N, w, prm=prm)
+        print(f"  {name:34s} t{w} {tw / 1e3:6.1f} ms  S({w}) = {t1 / tw:4.2f}", flush=True)
+
+
+COMMANDS = {"dist5": main_dist5, "one": main_one, "dist": main_dist, "seglen": main_seglen, "2d": main_2d, "cp": main_cp,
             "fastpanel": main_fastpanel, "waits": main_waits, "xcd": main_xcd}
 
 if __name__ == "__main__":
