@@ -917,6 +917,8 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
       FST(16);
+      // (a GE form over the k-steps from c0 / 4 only, fp64 storage, measured 119.8-120.2 vs
+      // 119.2-119.7 ms: not kept, profiles/r05/gepanel)
       apply_group<B, true, FLOW_PF, true, IB>(Vs, Tp, X, H, 0);
       FST(12);
       store_strip_pair<B, S>(X, Bt, ldm, col, h0);
