@@ -22,6 +22,10 @@ if [ "${C4:-0}" = 1 ]; then  # the 65536 x 16384 one-GPU line (the multi-GPU mod
   timeout -k 10 300 python bench.py --rows 65536 --cols 16384 --no-cpu-baseline --no-host-api > $OUT/bench_c4.json 2> $OUT/bench_c4.err || { echo "bench c4 failed"; tail -20 $OUT/bench_c4.err; exit 1; }
   cat $OUT/bench_c4.json
 fi
+if [ "${TIMELINE:-0}" = 1 ]; then  # the last steps' task timeline (stamps build libtqr_fst.so)
+  TQR_TIMELINE_TAIL=8 timeout -k 10 300 python tools/timeline.py 16384 256 > $OUT/timeline_f64.txt 2>&1 || { echo "timeline failed"; tail -20 $OUT/timeline_f64.txt; exit 1; }
+  head -24 $OUT/timeline_f64.txt
+fi
 if [ "${PROF:-1}" = 1 ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_f64 -o prof --output-format csv -- python3 bench.py --no-cpu-baseline --no-host-api --steps 3 --warmup 1 > $OUT/prof_f64.log 2>&1 || { echo "rocprof f64 failed"; tail -20 $OUT/prof_f64.log; exit 1; }
   find $OUT/prof_f64 -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-200 | head -5
