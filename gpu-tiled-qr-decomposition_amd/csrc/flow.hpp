@@ -784,12 +784,16 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
   }
   for (int g = 0; g < NG; ++g) {
     const int c0 = g * IB;
+#ifdef TQR_PANEL_LOAD_LATE  // (A/B: the block loaded after the previous member's Rr)
     if (!qrs) {  // R_kk rows of group g as left by the previous chain member
       FST(10);
       const bool ok = t == FLOW_PT ? spin_ge(&a.Rr[(size_t)k * NG + g], pos, a.err) : true;
       if (!wg_verdict(ok, sflag)) return;
       FST(1);
     }
+#endif
+    // the member's own block first: its columns depend on this member's own trailing update only,
+    // so its load overlaps the wait for the previous member's R rows of the group (Rr, below)
     {  // the group's B x IB block, row pairs as 16-B sc1 buffer loads (GEQRT: rows above c0 zero)
       const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(Bt + (size_t)c0 * ldm);  // offsets span IB columns
       const int rlo = qrs ? c0 : 0;
@@ -802,6 +806,14 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
         Vs[vimg_inv(r + 1) * VP + G::pc(c)] = v1;
       }
     }
+#ifndef TQR_PANEL_LOAD_LATE
+    if (!qrs) {  // R_kk rows of group g as left by the previous chain member
+      FST(10);
+      const bool ok = t == FLOW_PT ? spin_ge(&a.Rr[(size_t)k * NG + g], pos, a.err) : true;
+      if (!wg_verdict(ok, sflag)) return;
+      FST(1);
+    }
+#endif
     if (!qrs) {
       for (int idx = t; idx < IB * IB; idx += NT) {
         const int r = idx % IB, c = idx / IB;
