@@ -54,7 +54,7 @@ entry = {
 path = "profiles/pmc_summary.json"
 out = json.load(open(path)) if os.path.exists(path) else {}
 out["_doc"] = ("PMC summary of one k_flow launch per problem (tools/pmc_traffic.sh: rocprofv3 --pmc passes "
-               "over python3 bench.py --no-cpu-baseline --no-host-api --steps 1 --warmup 1, the last (warm) k_flow launch; CSVs under profiles/r05/final3/pmc*/). "
+               "over python3 bench.py --no-cpu-baseline --no-host-api --steps 1 --warmup 1, the last (warm) k_flow launch; CSVs under profiles/r05/final4/pmc*/). "
                + __doc__.split("\n", 2)[1].strip() + " See tools/pmc_summary.py for every formula.")
 out[key] = entry
 os.makedirs("profiles", exist_ok=True)
