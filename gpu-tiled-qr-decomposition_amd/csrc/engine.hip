@@ -19,6 +19,7 @@
 #include <map>
 #include <thread>
 #include <mutex>
+#include <string>
 #include <new>
 #include <tuple>
 #include <vector>
@@ -528,16 +529,30 @@ static double default_la(int dtype) { return dtype == TQR_F32 ? 2.0 : 0.0; }
 // (28 of 64 at 65536x16384) and the lookahead column's chains keyed 4 elements earlier. The model
 // with round-5 chain costs (tools/sched_sim.py dist5): S(8) 6.41 against 6.16 with
 // 2-element segments alone (tail 24 / 32: 6.35 / 6.39 with the keying, 6.38 at 32 without).
+// Round 6 calibrated the model against the one-GPU rehearsals (tools/sched_sim.py calib,
+// profiles/r06/model): measured / model 1.032-1.053 for 2 and 4 ranks; with that error the 8-GPU
+// time is 92.0-93.9 ms with these defaults against 95.6-97.6 ms with 2-element segments alone
+// (S(8) 6.19-6.32 vs 5.96-6.08), and the 4-rank rehearsal with these lists forced was predicted
+// slower (602.8 vs 572.0 ms model) and measured slower (621.8 vs 602.1 ms) — the model carries the
+// direction of the one-GPU cost; its 8-GPU gain (3.8 %) is a scale-free comparison of two lists
+// under the same error. The lone UNMQR segments do not follow the tail on these plans (the model:
+// no difference at 8 ranks, 89.2 ms either way): one-GPU plans only. TQR_DIST_DEFAULTS=r4 keeps the
+// round-4 list (2-element segments only) for an A/B on an 8-GPU node.
 struct MultiRankDefaults {
   int tail;
-  double lac;  // < 0: the panel keying (TQR_LA's default)
+  double lac;   // < 0: the panel keying (TQR_LA's default)
+  int ualone;   // < 0: follow the tail
 };
 static MultiRankDefaults multi_rank_defaults(int p, int q, int dtype, int world, bool full) {
   const int kmax = std::min(p, q);
-  if (world >= 4 && full) return {std::max(default_tail(p, q, dtype), 7 * kmax / 16), 4.0};
-  return {default_tail(p, q, dtype), -1.0};
+  const char* e = getenv("TQR_DIST_DEFAULTS");
+  const bool r4 = e && std::string(e) == "r4";
+  if (world >= 4 && full && !r4) return {std::max(default_tail(p, q, dtype), 7 * kmax / 16), 4.0, 0};
+  if (world > 1) return {default_tail(p, q, dtype), -1.0, 0};
+  return {default_tail(p, q, dtype), -1.0, -1};
 }
-static FlowKnobs knobs_from_env(int seglen, int tail_default = 0, double la_default = 0.0, double lac_default = -1.0) {
+static FlowKnobs knobs_from_env(int seglen, int tail_default = 0, double la_default = 0.0, double lac_default = -1.0,
+                                int ualone_default = -1) {
   FlowKnobs kn;
   kn.seglen = std::max(1, seglen);
   kn.tail = tail_default;
@@ -548,7 +563,7 @@ static FlowKnobs knobs_from_env(int seglen, int tail_default = 0, double la_defa
   kn.la_tail = e ? std::max(0, atoi(e)) : 0;
   if (const char* et = getenv("TQR_TAIL")) kn.tail = std::max(0, atoi(et));
   if (const char* ets = getenv("TQR_TAIL_SEGLEN")) kn.tail_sl = std::max(1, atoi(ets));
-  kn.ualone = kn.tail;
+  kn.ualone = ualone_default >= 0 ? ualone_default : kn.tail;
   if (const char* eua = getenv("TQR_UNMQR_ALONE")) kn.ualone = std::max(0, atoi(eua));
   if (const char* eg = getenv("TQR_TG")) kn.Tg = atof(eg);
   if (const char* el = getenv("TQR_LAZY")) kn.lazy = atof(el);
@@ -951,24 +966,43 @@ int tqr_plan_create_engine(tqr_plan** out, int m, int n, int b, int dtype, int e
   if (engine != TQR_ENGINE_DEFAULT && engine != TQR_ENGINE_WAVES && engine != TQR_ENGINE_FLOW) return TQR_EINVAL;
   return plan_create(out, m, n, b, dtype, 0, 1, engine);
 }
-// Multi-GPU plans raise the engine's wait limit (flow.hpp g_flow_wait_limit) for this process:
-// peers' launches may start seconds apart. TQR_PEER_TIMEOUT_S (default 60, at least 5).
-static int raise_wait_limit() {
-  static bool done = false;
-  if (done) return TQR_OK;
+// The engine's wait limit (flow.hpp g_flow_wait_limit, read only after a wait's first 5 s): 5 s for
+// one-GPU plans, TQR_PEER_TIMEOUT_S (default 60, at least 5) for multi-GPU plans, whose peers'
+// launches may start seconds apart. It is a per-device symbol, so every launch sets its plan's
+// value on its own stream when the device holds another one (a per-device cache skips the copy
+// otherwise): a one-GPU launch after a multi-GPU plan reports a real stall after 5 s again, and a
+// multi-GPU plan on any device gets its limit there. (Round 5 raised it once per process, on the
+// current device only.) Launches of plans with different limits running at once on one device
+// share whichever value was set last — only how long a real stall takes to be reported differs.
+static unsigned long long plan_wait_limit(int world) {
+  if (world <= 1) return FLOW_TIMEOUT;
   double sec = 60.0;
   if (const char* e = getenv("TQR_PEER_TIMEOUT_S")) sec = std::max(5.0, atof(e));
-  const unsigned long long ticks = (unsigned long long)(sec * 1e8);  // s_memrealtime: 100 MHz
-  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_flow_wait_limit), &ticks, sizeof(ticks)));
-  done = true;
+  return (unsigned long long)(sec * 1e8);  // s_memrealtime: 100 MHz
+}
+static int set_wait_limit(unsigned long long ticks, hipStream_t cs) {
+  constexpr int kDev = 64;
+  static std::mutex mu;
+  static unsigned long long cur[kDev] = {};  // per device: the value last set (0: unknown); also the
+                                             // copy's source, alive after the async copy returns
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kDev) {
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_flow_wait_limit), &ticks, sizeof(ticks)));
+    return TQR_OK;
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  if (cur[dev] == ticks) return TQR_OK;
+  cur[dev] = ticks;
+  if (hipMemcpyToSymbolAsync(HIP_SYMBOL(g_flow_wait_limit), &cur[dev], sizeof(ticks), 0, hipMemcpyHostToDevice, cs) !=
+      hipSuccess) {
+    cur[dev] = 0;
+    return TQR_EHIP;
+  }
   return TQR_OK;
 }
 int tqr_dist_plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world) {
   if (world < 1 || rank < 0 || rank >= world) return TQR_EINVAL;
-  if (world > 1) {
-    const int st = raise_wait_limit();
-    if (st) return st;
-  }
   return plan_create(out, m, n, b, dtype, rank, world, TQR_ENGINE_FLOW);
 }
 static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank, int world, int engine) {
@@ -1060,7 +1094,7 @@ static int plan_create(tqr_plan** out, int m, int n, int b, int dtype, int rank,
     if (const char* gs = getenv("TQR_FLOW_GRID")) pl->grid = std::max(1, atoi(gs));
     FlowPlan fp;
     const MultiRankDefaults mrd = multi_rank_defaults(pl->p, pl->q, dtype, world, pl->grid >= full_grid);
-    pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid), mrd.tail, default_la(dtype), mrd.lac);
+    pl->knobs = knobs_from_env(env_seglen(world, pl->grid >= full_grid), mrd.tail, default_la(dtype), mrd.lac, mrd.ualone);
     if (const char* eca = getenv("TQR_CHAIN_ASM")) pl->chain_asm = atoi(eca) & 3;  // 0 off, 1 on, 2 late strip loads
     // (bit 2: UNMQR elements on the full TSMQR bodies instead of the zero-row-skipping ones; A/B only)
     if (const char* eu = getenv("TQR_UNMQR_SKIP"); eu && atoi(eu) == 0 && pl->chain_asm) pl->chain_asm |= 4;
@@ -1346,15 +1380,19 @@ int tqr_dist_owner(const tqr_plan* pl, int tile_col) {
   return tile_owner(tile_col, pl->world, pl->cyclic);
 }
 
-// Host-only task-list helpers below describe the fp64 engine's list (flow_shape(TQR_F64)).
-static void host_flow_plan(int M, int N, int b, int seglen, FlowPlan& fp, const XferPlan* xp = nullptr) {
+// Host-only task-list helpers below describe the fp64 engine's list (flow_shape(TQR_F64)); world:
+// the ranks of a multi-GPU plan, each launch covering its whole device (the multi-rank defaults
+// apply as in tqr_dist_plan_create; the segment length is the caller's). M, N: tiles.
+static void host_flow_plan(int M, int N, int b, int seglen, FlowPlan& fp, const XferPlan* xp = nullptr, int world = 1) {
   const int sh = flow_shape(TQR_F64, b);
-  build_flow_plan(M, N, shape_ns(sh, b), b / shape_ib(sh, b), knobs_from_env(seglen, default_tail(M, N, TQR_F64)), fp, xp);
+  const MultiRankDefaults mrd = multi_rank_defaults(M, N, TQR_F64, world, true);
+  build_flow_plan(M, N, shape_ns(sh, b), b / shape_ib(sh, b),
+                  knobs_from_env(seglen, mrd.tail, default_la(TQR_F64), mrd.lac, mrd.ualone), fp, xp);
 }
 int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd) {
   if (M <= 0 || N <= 0 || !valid_b(b) || seglen < 1 || world < 1 || rank < 0 || rank >= world) return TQR_EINVAL;
   FlowPlan fp;
-  host_flow_plan(M, N, b, seglen, fp);
+  host_flow_plan(M, N, b, seglen, fp, nullptr, world);
   if (world > 1) partition_flow_plan(fp, rank, world);
   if (ntasks) *ntasks = (int)fp.items.size();
   if (nfwd) {  // panel members that forward their images (the panel tasks, when world > 1)
@@ -1513,6 +1551,7 @@ static int plan_execute(tqr_plan* pl, void* dA, int ldda, void* dtau, hipStream_
     }
     // local progress counters (multi-GPU: the member flags are epoch-valued and never reset)
     HIPCHK(hipMemsetAsync(pl->d_sync, 0, sizeof(int) * pl->sync_ints, cs));
+    if (const int st = set_wait_limit(plan_wait_limit(pl->world), cs)) return st;
     if (pl->profile) HIPCHK(hipEventRecord(pl->ev0, cs));
     hipLaunchKernelGGL(pl->kflow, dim3(pl->grid), dim3(pl->nt), pl->ldsF, cs, f);
     HIPCHK(hipGetLastError());

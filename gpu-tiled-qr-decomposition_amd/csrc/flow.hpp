@@ -83,6 +83,7 @@ extern __device__ unsigned long long g_wst[];
   } while (0)
 #define WST_MID() const unsigned long long wst1_ = __builtin_amdgcn_s_memrealtime(); WST_ACC(0, wst0_)
 #define WST_END() WST_ACC(1, wst1_)
+#define WST_ENDS(slot) WST_ACC(slot, wst1_)
 // group trace of workgroup 0 (stamps build): per group and wave, the s_memrealtime of marks
 // 0 loop top, 1 before the sync point, 2 after it, 3 phase 1 start, 4 phase 1 end, 5 head I/O end,
 // 6 phase 2 end (tools/group_trace.py)
@@ -110,6 +111,7 @@ __device__ constexpr int wmark_gtr(int slot) { return slot == 7 ? 0 : slot == 2 
 #define GTR(mark, tval) do {} while (0)
 #define WST_MID() do {} while (0)
 #define WST_END() do {} while (0)
+#define WST_ENDS(slot) do {} while (0)
 #endif
 // 512 threads = 8 waves = two waves per SIMD: a chain task updates a 128-column strip, so each
 // LDS-DMA'd V/T image serves twice the flops of the 4-wave / 64-column form, and each SIMD's

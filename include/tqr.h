@@ -151,7 +151,9 @@ int tqr_dist_local_cols(const tqr_plan* plan);
  * all reflector groups, to each of the world - 1 peers); 0 for a single-GPU plan */
 long long tqr_plan_fwd_bytes(const tqr_plan* plan);
 /* host-only: this rank's task-list length and the number of its panel members that forward
- * their V/T images to the peers (its panel tasks when world > 1, else 0) */
+ * their V/T images to the peers (its panel tasks when world > 1, else 0); the list is the one a
+ * plan of `world` ranks with a whole device each builds (the multi-rank task-list defaults of
+ * tqr_dist_plan_create apply; the segment length is `seglen`) */
 int tqr_dist_plan_check(int M, int N, int b, int seglen, int rank, int world, int* ntasks, int* nfwd);
 
 /* ---- one-shot helpers ------------------------------------------------------------------ */

@@ -29,13 +29,30 @@ def _free_port():
     return p
 
 
+def _global_list_len(M, N, b, world, monkeypatch):
+    """Tasks of the global list a plan of `world` whole-device ranks builds (engine.hip
+    multi_rank_defaults: 4+ ranks get one-element segments in the last 7/16 of the steps and the
+    lookahead column keyed 4 elements earlier; no rank's list has lone UNMQR segments)."""
+    kmax = min(M, N)
+    with monkeypatch.context() as mp:
+        if world >= 4:
+            tail = max(max(0, min(kmax, kmax - (M - 1 - 31))), 7 * kmax // 16)  # (default_tail)
+            mp.setenv("TQR_TAIL", str(max(0, tail)))
+            mp.setenv("TQR_TAIL_SEGLEN", "1")
+            mp.setenv("TQR_LAC", "4")
+        if world > 1:
+            mp.setenv("TQR_UNMQR_ALONE", "0")
+        return tqr.lib().tqr_flow_plan_export(M, N, b, 8, None, 0)
+
+
 @pytest.mark.parametrize("M,N", [(8, 8), (16, 4), (5, 7), (64, 64)])
-def test_partition_covers_global_list(M, N):
+def test_partition_covers_global_list(M, N, monkeypatch):
     b = 256
-    total, _ = tqr.dist_plan_check(M, N, b, 0, 1)
     kmax = min(M, N)
     npanel = sum(M - k for k in range(kmax))
+    assert tqr.dist_plan_check(M, N, b, 0, 1)[0] == _global_list_len(M, N, b, 1, monkeypatch)
     for world in (2, 3, 4, 8):
+        total = _global_list_len(M, N, b, world, monkeypatch)
         tasks = fwd = 0
         for r in range(world):
             nt, nf = tqr.dist_plan_check(M, N, b, r, world)
@@ -80,7 +97,7 @@ def _gloo_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_partition_gloo_world2():
+def test_partition_gloo_world2(monkeypatch):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -92,7 +109,7 @@ def test_partition_gloo_world2():
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
-    total, _ = tqr.dist_plan_check(32, 16, 256, 0, 1)
+    total = _global_list_len(32, 16, 256, 2, monkeypatch)
     npanel = sum(32 - k for k in range(16))
     for _, nt, nf in res:
         assert nf == npanel and nt == total

@@ -10,9 +10,14 @@ instantiation of flow_chain_asm:
   * no instruction outside an inline-asm block reads or writes a VGPR >= v32 (or an AGPR);
   * no scratch access between the first and the last inline-asm block (a spill reload would wait
     for the wave's whole memory queue), and no call anywhere.
+and, since round 6, the gfx950 hazard audit of every function with inline asm (tools/asm_hazards.py:
+every instruction pair in which one side is inline asm — inside the chain statements and across their
+boundaries with compiled code — against the wait-state table the generators pad with,
+gen/gfx950_hazards.py).
 Exit status 1 with the offending lines otherwise.
 Usage: check_chain_asm.py <device .s>
 """
+import os
 import re
 import sys
 
@@ -72,4 +77,8 @@ def check(path):
 
 
 if __name__ == "__main__":
-    sys.exit(check(sys.argv[1]))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import asm_hazards
+    rc_regs = check(sys.argv[1])
+    rc_hz = asm_hazards.main([sys.argv[1]])
+    sys.exit(1 if rc_regs or rc_hz else 0)

@@ -46,7 +46,11 @@ for c in range(NC):
 WSL = 8
 ws = (ctypes.c_ulonglong * (8 * WSL * nb))()  # (g_wst holds 8 wave slots per workgroup)
 if hasattr(L, "tqr_debug_flow_wave_stamps") and L.tqr_debug_flow_wave_stamps(ws, nb) == 0:
-    wn = ["drain", "barrier", "pre-sync", "post-sync", "phase1", "head I/O", "phase2", "tail"]
+    # (the asm chains: "phase1" is the whole group statement, slot 5 the task-start dependency wait
+    # (spins + barrier), slot 6 the task end (element end, drain barrier, publishes))
+    asm = os.environ.get("TQR_CHAIN_ASM", "2") != "0"
+    wn = ["drain", "barrier", "pre-sync", "post-sync", "body" if asm else "phase1", "tstart" if asm else "head I/O",
+          "tend" if asm else "phase2", "tail"]
     print("  per-wave sums (ms/WG): " + " | ".join(f"{n:>9s}" for n in wn))
     for w in range(NW):
         v = [sum(ws[b * 8 * WSL + WSL * w + c] for b in range(nb)) / nb / 1e5 for c in range(WSL)]

@@ -320,6 +320,12 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
                 r = (j + (kk >> 16)) % world
         hp = pheaps[r] if (pres and typ != 4) else heaps[r]
         t0 = heapq.heappop(hp) + prm["disp"]
+        # split panel (what-if, prm["split_from"]): steps >= it run a member as two co-scheduled
+        # tasks, F (factorisation, block in / R, V out) and U (T, images, in-tile trailing update): U
+        # updates the next group's block first (prm["u"] us after T), so F's next group starts then
+        split = typ != 4 and kk >= prm.get("split_from", 1 << 30) and (not prm.get("split_ge") or l == kk)
+        if split:
+            t0u = heapq.heappop(hp) + prm["disp"]
         if typ != 4:
             t = t0
             if k > 0:
@@ -329,6 +335,8 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
             prev = (i - 1, k) if i > k else None
             for g in range(NG):
                 gs = t if g == 0 else ee[g - 1]
+                if split and g > 0:
+                    gs = rr[g - 1] + prm["bt"] + prm.get("u", 6.0) + prm["io_in"]
                 if prev:
                     gs = max(gs, FS[prev][g] + fine[0]) if fine else max(gs, Rr[prev][g])
                 fs[g] = gs
@@ -356,6 +364,10 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
             Rr[(i, k)], Rc[(i, k)], E[(i, k)], FL[(i, k)] = rr, rc, ee, fl
             FS[(i, k)] = fs
             end = ee[-1]
+            if split:  # F's workgroup is free after its last write-back, U's after the last trailing
+                heapq.heappush(hp, rr[-1])
+                span = max(span, rr[-1])
+                t0 = max(t0, t0u)
         else:
             s = (ts >> 8) & 0xff
             i0, i1 = l & 0xffff, l >> 16
@@ -770,7 +782,74 @@ def main_dist5(argv):
         print(f"  {name:34s} t{w} {tw / 1e3:6.1f} ms  S({w}) = {t1 / tw:4.2f}", flush=True)
 
 
-COMMANDS = {"dist5": main_dist5, "one": main_one, "dist": main_dist, "seglen": main_seglen, "2d": main_2d, "cp": main_cp,
+def main_split(argv):
+    """One GPU, round-5 costs: the panel member split into a factorisation task and an update task
+    (F / U, U updating the next group's block first) for the steps >= S. Args: [M] [S ...]"""
+    M = int(argv[0]) if argv else 64
+    prm = dict(P5, f=29.6, bt=10.6, t=15.9, io_in=4.0, io_wb=4.0, io_img=4.3)
+    items = export_list(M, M, seglen=8)
+    base = simulate_dist(items, M, M, 1, prm=prm)
+    print(f"{M}x{M} tiles, round-5 costs, panel group cycle "
+          f"{prm['io_in'] + prm['f'] + prm['io_wb'] + prm['bt'] + prm['io_img'] + prm['t']:.1f} us: {base / 1e3:.2f} ms")
+    for sf in [int(x) for x in argv[1:]] or [0, M // 4, M // 2, 3 * M // 4]:
+        for u in (6.0, 10.0):
+            t = simulate_dist(items, M, M, 1, prm=dict(prm, split_from=sf, u=u))
+            print(f"  split from step {sf:3d}, next block {u:4.1f} us after T: {t / 1e3:7.2f} ms ({(t - base) / 1e3:+.2f})")
+
+
+def _list_env(env, M, N):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return export_list(M, N, seglen=int(os.environ.get("TQR_SEGLEN", "8")))
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
+
+
+# the round-5 one-GPU measurements at 65536 x 16384 (BASELINE configs[3], profiles/r05/reh5): ranks x
+# workgroups per rank, task list, measured ms per factorisation. The rehearsals share one GPU.
+REH5 = [("1 rank x 256 (one GPU, c4)", 1, 256, "r4", 581.338),
+        ("1 rank x 128 (t1 leg of the 2-rank run)", 1, 128, "r4", 1083.162),
+        ("1 rank x 64 (t1 leg of the 4-rank run)", 1, 64, "r4", 2081.133),
+        ("1 rank x 64, 8-GPU list (t1 leg)", 1, 64, "r5", 2191.254),
+        ("2 ranks x 128 (rehearsal)", 2, 128, "r4", 591.792),
+        ("4 ranks x 64 (rehearsal)", 4, 64, "r4", 602.1),
+        ("4 ranks x 64, 8-GPU list (rehearsal)", 4, 64, "r5", 621.778)]
+LISTS = {"r4": {"TQR_SEGLEN": "8"},  # (the rehearsals' ranks do not cover a device: segment length 8)
+         "r4d": {"TQR_SEGLEN": "2"},  # round-4 multi-rank default: 2-element segments
+         "r5": {"TQR_SEGLEN": "2", "TQR_TAIL": "28", "TQR_TAIL_SEGLEN": "1", "TQR_LAC": "4"}}  # round 5's
+
+
+def main_calib(argv):
+    """The multi-GPU model against the round-5 one-GPU measurements (profiles/r05/reh5): per shape the
+    model's time, the measured one, their ratio; then t(8) on 8 x 256 workgroups for the round-4 and
+    round-5 multi-rank task lists, corrected by the rehearsals' fitted ratio. Args: [M] [N]"""
+    M, N = _mn(argv)
+    seg = float(os.environ.get("TQR_SIM_SEG", "20"))
+    prm = dict(P5, seg=seg)
+    lists = {k: _list_env(v, M, N) for k, v in LISTS.items()}
+    ratios = {}
+    print(f"{M}x{N} tiles, round-5 costs, per-segment {seg} us", flush=True)
+    for name, world, W, lst, meas in REH5:
+        t = simulate_dist(lists[lst], M, N, world, prm=dict(prm, W=W)) / 1e3
+        ratios[name] = meas / t
+        print(f"  {name:42s} model {t:8.1f} ms  measured {meas:8.1f}  ratio {meas / t:5.3f}", flush=True)
+    reh = [ratios[n] for n, w, *_ in REH5 if w > 1]
+    one = ratios[REH5[0][0]]
+    lo, hi = min(reh), max(reh)
+    print(f"  multi-rank rehearsals: measured / model {lo:.3f} .. {hi:.3f}; one GPU {one:.3f}")
+    t1 = REH5[0][4]
+    for lst in ("r4d", "r5"):
+        t8 = simulate_dist(lists[lst], M, N, 8, prm=dict(prm, W=256)) / 1e3
+        print(f"  8 x 256, list {lst:3s}: model t(8) {t8:6.1f} ms, S(8) {t1 / t8:4.2f} uncorrected; corrected t(8) "
+              f"{t8 * lo:6.1f} .. {t8 * hi:6.1f} ms, S(8) {t1 / (t8 * hi):4.2f} .. {t1 / (t8 * lo):4.2f}", flush=True)
+
+
+COMMANDS = {"calib": main_calib, "split": main_split, "dist5": main_dist5, "one": main_one, "dist": main_dist, "seglen": main_seglen, "2d": main_2d, "cp": main_cp,
             "fastpanel": main_fastpanel, "waits": main_waits, "xcd": main_xcd}
 
 if __name__ == "__main__":

@@ -26,6 +26,9 @@ items = (ctypes.c_int * (4 * n))()
 assert L.tqr_debug_task_timeline(p.h, tl, n, items) == 0
 T = np.frombuffer(tl, dtype=np.uint64).reshape(n, 3).astype(np.int64)
 I = np.frombuffer(items, dtype=np.int32).reshape(n, 4)
+# (the fp64 asm chain adds its start's dependency wait in bits 16.. of the workgroup word)
+Wst = (T[:, 2] >> 16) / 100.0  # us
+T[:, 2] &= 0xffff
 if os.environ.get("TQR_TIMELINE_DUMP"):
     np.savez_compressed(os.environ["TQR_TIMELINE_DUMP"], T=T, I=I)
 t0 = T[:, 0].min()
@@ -43,6 +46,13 @@ for kk in list(range(0, K, max(1, K // 16))) + [K - 1]:
     ps = f"{s[pm].min() / 1e3:7.2f}..{e[pm].max() / 1e3:7.2f}" if pm.any() else "   -   "
     cs = f"{s[cm].min() / 1e3:7.2f}..{e[cm].max() / 1e3:7.2f}" if cm.any() else "   -   "
     print(f" {kk:4d}  {ps}        {cs}      {cm.sum():5d}")
+if Wst.any():
+    print(" chain tasks' start wait (dependency spins + barrier), per step range:")
+    for lo in range(0, K, max(1, K // 8)):
+        cm = chain & (k >= lo) & (k < lo + max(1, K // 8))
+        if cm.any():
+            print(f"   steps {lo:3d}..{lo + max(1, K // 8) - 1:3d}: {cm.sum():6d} tasks, mean {Wst[cm].mean():7.1f} us, "
+                  f"total {Wst[cm].sum() / grid.value / 1e3:6.2f} ms per workgroup")
 # workgroups holding a task, per 5 % of the span
 span = e.max()
 print(" occupancy (mean workgroups holding a task) per 5 % of the launch:")
