@@ -160,7 +160,7 @@ class Insn:
         elif op.startswith("s_"):
             self.cls = "salu"
             if op.startswith(("s_cmp", "s_bitcmp", "s_waitcnt", "s_barrier", "s_setprio", "s_sleep", "s_sendmsg",
-                              "s_set_gpr_idx_off", "s_dcache", "s_icache", "s_trap", "s_ttrace")):
+                              "s_set_gpr_idx_off", "s_icache", "s_trap", "s_ttrace")):
                 for i in range(n):
                     self._r(i, "salu")
             else:
