@@ -213,8 +213,8 @@ def _required(w_cls, w_op, reg, insn, role, hw=False, w_d=None):
             return t["srcc"] if role == "srcc" else t["srcab"]
         if insn.cls in ("valu", "readlane"):
             return t["valu"]
-        if role == "store_data":
-            return t["vmem"]
+        if role == "store_data" or insn.cls in ("ds", "load", "store", "lds_dma"):
+            return t["vmem"]  # (as VMEM / LDS data or address: ds_bpermute of the strip, ds_write of a result)
         return 0
     if w_cls in ("valu", "readlane"):
         if vec:

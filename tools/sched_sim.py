@@ -347,6 +347,12 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
                 if prev and fine:
                     rr[g] = max(rr[g], Rr[prev][g] + fine[0])
                 rc[g] = rr[g] + prm["bt"] + prm["io_img"]
+                # what-if (prm["rc_late"]: "ge" GEQRT only / "all"): the images stored before the
+                # trailing update but published with Rt after its drain — the image drain leaves the
+                # member's group cycle, Rc comes t later
+                late = prm.get("rc_late") == "all" or (prm.get("rc_late") == "ge" and i == k)
+                if late:
+                    rc[g] = rr[g] + prm["bt"] + prm.get("io_img_issue", 1.5)
                 last = g + 1 == NG
                 inline = world > 1 and (mode == "inline" or last)
                 ready = rc[g] + (fw if inline else 0.0)
@@ -354,6 +360,8 @@ def simulate_dist(items, M, N, world, ns=2, prm=P, fwd_peer=1.6, hop=3.0, mode="
                     ee[g] = max(ready + prm["t"], E[prev][g] + fine[1])
                 else:
                     ee[g] = (max(ready, E[prev][g]) if prev else ready) + prm["t"]
+                if late:
+                    rc[g] = ee[g]
                 if world > 1:
                     if inline:
                         fl[g] = ee[g] + hop

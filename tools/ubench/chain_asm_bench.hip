@@ -86,6 +86,9 @@ __global__ __launch_bounds__(512, 1) void k_asm(double* X0, double* H0, const do
       o.vt = vb + ot;
       o.vl16 = vl16;
       o.loff = loff;
+      o.bpa = coal_bpa(lane);  // (used by GEN_COALESCE bodies only)
+      o.loffc = coal_off(lane, ldm);
+      o.hoff = __builtin_amdgcn_readfirstlane((int)(8 * ldm * 8));
       o.svsrc = vimg(0, 0);
       o.stsrc = vimg(0, 0) + G::VIMG;
       o.sdst = sreg(lds0 + (unsigned)((buf ^ 1) * BUF * 8));
@@ -129,6 +132,9 @@ __global__ __launch_bounds__(512, 1) void k_asm(double* X0, double* H0, const do
       o.vt = vb + ot;
       o.vl16 = vl16;
       o.loff = loff;
+      o.bpa = coal_bpa(lane);  // (used by GEN_COALESCE bodies only)
+      o.loffc = coal_off(lane, ldm);
+      o.hoff = __builtin_amdgcn_readfirstlane((int)(8 * ldm * 8));
       o.svsrc = vimg(id, gd);
       o.stsrc = vimg(id, gd) + G::VIMG;
       o.sdst = sreg(lds0 + (unsigned)((buf ^ 1) * BUF * 8));
@@ -229,6 +235,9 @@ __global__ __launch_bounds__(256, 1) void k_asm4(double* X0, double* H0, const d
       o.vt = vb + ot;
       o.vl16 = vl16;
       o.loff = loff;
+      o.bpa = coal_bpa(lane);  // (used by GEN_COALESCE bodies only)
+      o.loffc = coal_off(lane, ldm);
+      o.hoff = __builtin_amdgcn_readfirstlane((int)(8 * ldm * 8));
       o.svsrc = vimg(id, gd);
       o.stsrc = vimg(id, gd) + G::VIMG;
       o.sdst = sreg(lds0 + (unsigned)((buf ^ 1) * BUF * 8));

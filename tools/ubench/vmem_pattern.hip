@@ -30,6 +30,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
 // MODE 1 = stores, 2 = loads, 3 = both (store p, then load p - 2); REP elements back to back.
 // +4: full-line layout (each instruction 8 columns x 128 B: lane (x, c) -> column c & 7 (+8 for odd
 // instructions), rows 16 (p/2) + 2x + 8 (c >= 8)), +8: contiguous (1 KiB per instruction in one column)
+// Round 6, the strip's own 16 x 256 geometry with fewer columns per instruction (the same bytes):
+// +16: 1 column per instruction (1 KiB = 128 rows), +32: 4 columns x 256 B, +64: 8 columns x 128 B,
+// +128: the strip's own 16 columns x 64 B per instruction, but the 4 lanes of a column consecutive;
+// +256 / +512: the strip layout moved by ds_bpermute to +128's / to 8 columns x 128 B (stores only)
 template <int MODE, int SAUX = 16>
 __global__ __launch_bounds__(512, 1) void k_io(double* X, long ldm, int rep, unsigned long long* clk) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63, x = lane >> 4, c = lane & 15;
@@ -49,10 +53,41 @@ __global__ __launch_bounds__(512, 1) void k_io(double* X, long ldm, int rep, uns
     double* base = X + (size_t)(blockIdx.x * 128 + 16 * w) * ldm + (size_t)(e % 32) * 256;
     const __amdgpu_buffer_rsrc_t so = rsrc(base), si = rsrc(base + 256);
     auto o = [&](int p) {
+      if (MODE & 128) return (unsigned)(((size_t)(lane >> 2) * ldm + 8 * p + 2 * (lane & 3)) * 8);
+      if (MODE & 16) return (unsigned)((size_t)(p / 2) * ldm * 8 + (p % 2) * 1024 + lane * 16);
+      if (MODE & 32) return (unsigned)(((size_t)(4 * (p % 4) + lane / 16) * ldm + 32 * (p / 4) + 2 * (lane % 16)) * 8);
+      if (MODE & 64) return (unsigned)(((size_t)(8 * (p % 2) + lane / 8) * ldm + 16 * (p / 2) + 2 * (lane % 8)) * 8);
       if (MODE & 8) return (unsigned)(p * 1024 + ((p & 1) ? 0 : 0)) + off + (unsigned)(w * 0);
       if (MODE & 4) return ((p & 1) ? off2 : off) + 128u * (p >> 1);
       return off + 64u * p;
     };
+    if constexpr ((MODE & 256) != 0) {  // strip layout -> 16 columns x 64 B, 4 consecutive lanes per column
+      const int src = (((lane & 3) << 4) | (lane >> 2)) * 4;
+      const unsigned oq = (unsigned)(((size_t)(lane >> 2) * ldm + 2 * (lane & 3)) * 8);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        v4u v;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) v[d] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)r[p][d]);
+        __builtin_amdgcn_raw_buffer_store_b128(v, so, oq + 64u * p, 0, SAUX);
+      }
+    } else if constexpr ((MODE & 512) != 0) {  // strip layout -> 8 columns x 128 B (two row pairs), 8 lanes per column
+      const int c1 = lane >> 3, r1 = lane & 7;
+#pragma unroll
+      for (int q = 0; q < NP / 2; ++q)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int src = (((r1 & 3) << 4) | ((2 * h + (c1 >> 2)) << 2) | (c1 & 3)) * 4;
+          v4u v;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            const unsigned a = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)r[2 * q][d]);
+            const unsigned b = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)r[2 * q + 1][d]);
+            v[d] = (r1 & 4) ? b : a;
+          }
+          __builtin_amdgcn_raw_buffer_store_b128(v, so, (unsigned)(((size_t)(8 * h + c1) * ldm + 16 * q + 2 * r1) * 8), 0, SAUX);
+        }
+    } else
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       if (MODE & 1) __builtin_amdgcn_raw_buffer_store_b128(r[p], so, o(p), 0, SAUX);
@@ -84,7 +119,8 @@ static int run(double* X, long ldm, int nwg, int rep, unsigned long long* clk) {
   const double kib = ((MODE & 3) == 3 ? 2.0 : 1.0) * NP * 8;  // KiB per workgroup per element
   printf("aux %2d mode %2d (%s, %s) %3d WG: %.2f us per element per WG, %.1f GB/s per CU\n", SAUX, MODE,
          (MODE & 3) == 1 ? "stores" : (MODE & 3) == 2 ? "loads " : "both  ",
-         (MODE & 8) ? "contiguous" : (MODE & 4) ? "full lines" : "half lines", nwg, us, kib * 1024 / us / 1e3);
+         (MODE & 256) ? "bperm->quad" : (MODE & 512) ? "bperm->line" : (MODE & 128) ? "16x64B quad" : (MODE & 16) ? "1 col/insn" : (MODE & 32) ? "4 col/insn" : (MODE & 64) ? "8 col/insn" : (MODE & 8) ? "contiguous"
+         : (MODE & 4) ? "full lines" : "half lines", nwg, us, kib * 1024 / us / 1e3);
   return 0;
 }
 
@@ -99,6 +135,23 @@ int main(int argc, char** argv) {
   CK(hipMemset(X, 0, (size_t)ncu * 128 * ldm * 8));
   unsigned long long* clk;
   CK(hipMalloc(&clk, sizeof(unsigned long long) * 1024));
+  if (argc > 2 && atoi(argv[2]) == 2) {  // columns per instruction (round 6)
+    for (int nwg : {1, ncu}) {
+      if (run<1 + 128>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<1 + 256>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<1 + 512>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<3 + 128>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<1>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<1 + 64>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<1 + 32>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<1 + 16>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<3>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<3 + 64>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<3 + 32>(X, ldm, nwg, rep, clk)) return 1;
+      if (run<3 + 16>(X, ldm, nwg, rep, clk)) return 1;
+    }
+    return 0;
+  }
   if (argc > 2) {  // store cache-policy sweep
     for (int nwg : {1, ncu}) {
       if (run<1, 0>(X, ldm, nwg, rep, clk)) return 1;
