@@ -48,9 +48,13 @@ __device__ __forceinline__ f4v ld_f4(__amdgpu_buffer_rsrc_t rs, unsigned off) {
 // Panel side: the fp32 chain's images of one reflector group from the panel's fp64 LDS block (rows
 // in the paired order of flow_panel: tile row R at LDS row vimg_inv(R), columns permuted by pc) and
 // its T (row-major, pitch TP). All panel threads; 16-B write-through stores.
+// lvr / ltp (LDS, optional): the same chunks, for the panel's own trailing update (flow_panel)
+typedef __attribute__((address_space(3))) f4v lds_f4_t;
 template <int B>
 __device__ __noinline__ void write_images32(const double* Vs, const double* Ts, __amdgpu_buffer_rsrc_t rv,
-                                            __amdgpu_buffer_rsrc_t rt) {
+                                            __amdgpu_buffer_rsrc_t rt, float* lvr, float* ltp) {
+  lds_f4_t* const lv = lvr ? (lds_f4_t*)(const __attribute__((address_space(3))) void*)lvr : nullptr;
+  lds_f4_t* const lt = ltp ? (lds_f4_t*)(const __attribute__((address_space(3))) void*)ltp : nullptr;
   using G = Geo<B>;
   using G32 = Geo32<B>;
   constexpr int NMI = G32::NMI, VP = G::VP, TP = G::TP;
@@ -64,6 +68,7 @@ __device__ __noinline__ void write_images32(const double* Vs, const double* Ts, 
       v[e] = V(R, 16 * wi + 4 * x + r);
     }
     st_f4(rv, 16u * idx, v);
+    if (lv) lv[idx] = v;
   }
   for (int idx = threadIdx.x; idx < G32::TIMG * 2 / 4; idx += blockDim.x) {  // TP chunks (+ zero pad)
     const int lane = idx & 63, pr = idx >> 6, x = lane >> 4, y = lane & 15;
@@ -77,6 +82,7 @@ __device__ __noinline__ void write_images32(const double* Vs, const double* Ts, 
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = pr < G32::NPR ? (float)(-Ts[(16 * mi + 4 * x + r) * TP + 16 * wi + sig16(y)]) : 0.0f;
     st_f4(rt, 16u * idx, v);
+    if (lt) lt[idx] = v;
   }
 }
 
@@ -272,6 +278,44 @@ struct Strip32 {
   }
   __device__ __forceinline__ unsigned off(int mt) const { return base + 64u * mt; }
 };
+
+// fp32 storage: the panel group's in-tile trailing update in fp32 on v_mfma_f32_16x16x4_f32 (the
+// chains' arithmetic and the reference's own precision, qrdecomp.c:559-763 in float), twice the
+// fp64 4x4x4 form's rate, from the group's fp32 images that write_images32 also left in LDS (VRl,
+// then the packed -T). Until round 5 the panel applied its fp64 V / T on the fp64 MFMA (what-if
+// without the trailing update: -17.6 ms at 32768^2, profiles/r06/whatif_f32.txt). Wave w takes the
+// 16-column strips w, w + nw, ... right of the group. GEQRT (qrs): the tiles above the group are
+// neither loaded nor stored (finished R rows, which the next member's trailing may be updating) and
+// the GE V's zero tiles are skipped (apply32_ge); TSQRT: R_kk's rows of the group are the head.
+template <int B>
+__device__ __noinline__ void panel_trail32(float* Bt, float* Rt, size_t ldm, bool qrs, int g, int c0, int nstr,
+                                           const float* VRl, int nw) {
+  using G32 = Geo32<B>;
+  constexpr int NMT = G32::NMT, NMI = G32::NMI;
+  const float* TPl = VRl + G32::VR;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int mt0 = qrs ? c0 / 16 : 0;
+  for (int s = w; s < nstr; s += nw) {
+    const int col = c0 + G32::IB + 16 * s;
+    const Strip32<B> xs(Bt, ldm, col);
+    f4v X[NMT], Hg[NMT];
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt) X[mt] = mt >= mt0 ? ld_f4(xs.rs, xs.off(mt)) : f4v{0.f, 0.f, 0.f, 0.f};
+    if (qrs) {
+      apply32_ge<B>(g, VRl, TPl, X, NoHook());
+    } else {
+      const Strip32<B> hs(Rt, ldm, col);
+#pragma unroll
+      for (int mi = 0; mi < NMI; ++mi) Hg[mi] = ld_f4(hs.rs, hs.off(c0 / 16 + mi));
+      apply32<B, true, NoHook>(VRl, TPl, X, Hg, NoHook());
+#pragma unroll
+      for (int mi = 0; mi < NMI; ++mi) st_f4(hs.rs, hs.off(c0 / 16 + mi), Hg[mi]);
+    }
+#pragma unroll
+    for (int mt = 0; mt < NMT; ++mt)
+      if (mt >= mt0) st_f4(xs.rs, xs.off(mt), X[mt]);
+  }
+}
 
 template <int B>
 __device__ __noinline__ void flow_chain32(const FlowArgs& a, int s_, int i0_, int i1_, int j_, int k_, int seg_,

@@ -644,10 +644,14 @@ __device__ __forceinline__ void st_pair(__amdgpu_buffer_rsrc_t rs, unsigned off,
   }
 }
 
-// the fp32 chain's operand images of one group (chain32.hpp)
+// the fp32 chain's operand images of one group (chain32.hpp), optionally also into LDS
 template <int B>
 __device__ __noinline__ void write_images32(const double* Vs, const double* Ts, __amdgpu_buffer_rsrc_t rv,
-                                            __amdgpu_buffer_rsrc_t rt);
+                                            __amdgpu_buffer_rsrc_t rt, float* lvr = nullptr, float* ltp = nullptr);
+// fp32 storage: a panel group's in-tile trailing update on the fp32 MFMA (chain32.hpp)
+template <int B>
+__device__ __noinline__ void panel_trail32(float* Bt, float* Rt, size_t ldm, bool qrs, int g, int c0, int nstr,
+                                           const float* VRl, int nw);
 
 // Multi-GPU: the panel task itself copies each group's V and T images from its workspace slot
 // into every peer's (16-B system-scope stores over xGMI), right after the group's Rc publish;
@@ -740,6 +744,22 @@ __device__ __noinline__ void panel_idle(const FwdJob* fjp, int IB, bool TS) {
 }
 
 // ---- panel tasks ---------------------------------------------------------------------------
+// LDS of a panel task (doubles): V block Vs, head / T / Gram images Hs Ts Gs, tau, then the
+// factorisation's scratch and build_t's partial Grams Gp (flow_panel). fp32 storage keeps the
+// group's fp32 chain images (Geo32 VR floats, then the packed -T chunks) for its in-tile trailing
+// update in that scratch + Gp region, dead by then (flow_panel_img32_at)
+template <int B, class C>
+constexpr int flow_panel_doubles() {
+  using G = FGeo<B, C>;
+  return G::VSZ + 8 * G::TSZ + G::IB + 2 + 2 * 4 * 32 + 4 * 32 + 2 * 32;
+}
+template <int B, class C>
+constexpr int flow_panel_img32_at() {
+  using G = FGeo<B, C>;
+  constexpr int at = G::VSZ + 3 * G::TSZ + G::IB + 2;  // = scratch
+  static_assert(at + Geo32<B>::VR / 2 + Geo32<B>::TIMG <= flow_panel_doubles<B, C>(), "fp32 images in the panel's LDS");
+  return at;
+}
 template <int B, typename S, class C>
 __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int k, double* lds, int* sflag) {
   using G = FGeo<B, C>;
@@ -864,6 +884,9 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     }
     FST(10);
 #ifndef TQR_DIAG_NOBT  // what-if: no T formation (results wrong)
+#ifdef TQR_DIAG_GEFAST  // what-if: GEQRT without T formation and in-tile trailing update (results wrong)
+    if (!qrs)
+#endif
     build_t<B, IB>(Vs, tauv, Gs, Ts, Gp, 0);  // (permuted rows: the GE zero rows are not a prefix)
 #endif
     // packed T (the Gram buffer is free now): the trailing update's and the chains' T operand
@@ -890,7 +913,9 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
         for (int idx = t; idx < G::TPIMG / 2; idx += NT) st_pair<double>(rt, 16 * idx, tpk(2 * idx), tpk(2 * idx + 1));
         for (int idx = t; idx < G::VSZ / 2; idx += NT) st_pair<double>(rv, 16 * idx, vim(2 * idx), vim(2 * idx + 1));
       } else {
-        write_images32<B>(Vs, Ts, rv, rt);  // the fp32 chain's operand images (chain32.hpp)
+        // the fp32 chain's operand images (chain32.hpp), kept in LDS for this group's trailing update
+        write_images32<B>(Vs, Ts, rv, rt, (float*)(lds + flow_panel_img32_at<B, C>()),
+                          (float*)(lds + flow_panel_img32_at<B, C>() + Geo32<B>::VR / 2));
       }
     }
     // group factorised: R diagonal block, V, tau, images out -> next member and the chains go
@@ -916,10 +941,23 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
     // updating meanwhile); the head resource is empty for GEQRT (loads 0, stores dropped) —
     // see flow_chain's UNMQR element.
     const int h0 = qrs ? c0 / 8 : 0;
+#ifndef TQR_PANEL_TRAIL64_F32  // (A/B: fp32 storage's trailing update in fp64 on the 4x4x4 MFMA, as until round 5)
+    constexpr bool trail32 = sizeof(S) == 4 && C::NW == 8;
+#else
+    constexpr bool trail32 = false;
+#endif
+    if constexpr (trail32) {
+      // fp32 storage: the in-tile trailing update in fp32 on the fp32 MFMA (chain32.hpp panel_trail32)
+      __syncthreads();  // (every wave's LDS image writes)
+      panel_trail32<B>((float*)Bt, (float*)Rt, ldm, qrs, g, c0, nstr,
+                       (const float*)(lds + flow_panel_img32_at<B, C>()), C::NW);
+    }
 #ifdef TQR_DIAG_NOPTRAIL  // what-if: no in-tile trailing update (results wrong)
     for (int s = nstr; s < nstr; s += C::NW) {
+#elif defined(TQR_DIAG_GEFAST)
+    for (int s = qrs ? nstr : w; s < nstr; s += C::NW) {
 #else
-    for (int s = w; s < nstr; s += C::NW) {
+    for (int s = trail32 ? nstr : w; s < nstr; s += C::NW) {
 #endif
       asm volatile("" ::: "memory");
       const int col = c0 + IB + 16 * s;
@@ -935,7 +973,11 @@ __device__ __noinline__ void flow_panel(const FlowArgs& a, int type, int l, int 
       // 119.2-119.7 ms: not kept, profiles/r05/gepanel)
       apply_group<B, true, FLOW_PF, true, IB>(Vs, Tp, X, H, 0);
       FST(12);
-      store_strip_pair<B, S>(X, Bt, ldm, col, h0);
+#ifndef TQR_PANEL_STRIP_PLAIN  // (A/B: the MFMA-layout stores)
+      if constexpr (sizeof(S) == 8) store_strip_coal<B>(X, (double*)Bt, ldm, col, h0);
+      else
+#endif
+        store_strip_pair<B, S>(X, Bt, ldm, col, h0);
       store_head_buf<B, S, 16, IB>(H, rsH, so);
       FST(17);
     }
@@ -1319,8 +1361,7 @@ namespace tqr {
 // dynamic LDS (doubles) of the task paths; the LDS tail (task word, verdicts, ...) follows
 template <int B, typename S, class C>
 constexpr int flow_lds_doubles() {
-  using G = FGeo<B, C>;
-  constexpr int panel = G::VSZ + 8 * G::TSZ + G::IB + 2 + 2 * 4 * 32 + 4 * 32 + 2 * 32;
+  constexpr int panel = flow_panel_doubles<B, C>();
   constexpr int chain = 2 * (FImg<B, S, C>::V + FImg<B, S, C>::T);
   return panel > chain ? panel : chain;
 }

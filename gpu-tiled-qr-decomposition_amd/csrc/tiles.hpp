@@ -522,6 +522,45 @@ __device__ __forceinline__ void store_strip_pair(const double (&X)[Geo<B>::NKS],
     }
   }
 }
+// The same fp64 strip stored as full 128-B lines by 8 consecutive lanes (round 6): the MFMA layout
+// above puts a column's four lanes 16 apart, and the CU's store path does not merge lanes that are
+// not adjacent — 256 KiB per CU of strip stores take 7.1 us that way and 3.0 us with the row pairs
+// first moved across lanes by ds_bpermute (tools/ubench/vmem_pattern.hip, profiles/r06/vmem/).
+// Store q, half h: lane L = 8 c + r writes column 8 h + c, rows 16 q + 2 r, + 1 — row pair 2 q + (r >> 2)
+// of lane ((r & 3) << 4) | (8 h + c). Loads need no such move (they merge at any lane order).
+template <int B>
+__device__ __forceinline__ void store_strip_coal(const double (&X)[Geo<B>::NKS], double* tile, size_t ldm, int col0,
+                                                 int h0 = 0) {
+  const int lane = threadIdx.x & 63, c = lane >> 3, r = lane & 7;
+  __amdgpu_buffer_rsrc_t rs = uniform_rsrc(tile + (size_t)col0 * ldm);
+  const unsigned base = (unsigned)(((size_t)c * ldm + 2 * r) * sizeof(double));
+  const int hoff = __builtin_amdgcn_readfirstlane((int)(8 * ldm * sizeof(double)));
+  const int src = 4 * (((r & 3) << 4) | c);
+  const bool hi = (r & 4) != 0;
+  typedef __attribute__((ext_vector_type(4))) unsigned v4u;
+#pragma unroll
+  for (int q = 0; q < Geo<B>::NKS / 4; ++q) {
+    if (2 * q < h0) continue;  // (h0 even: the GEQRT panel's 8-row blocks above its group)
+    unsigned w0[4], w1[4];
+    const unsigned long long a0 = (unsigned long long)__double_as_longlong(X[4 * q]);
+    const unsigned long long a1 = (unsigned long long)__double_as_longlong(X[4 * q + 1]);
+    const unsigned long long b0 = (unsigned long long)__double_as_longlong(X[4 * q + 2]);
+    const unsigned long long b1 = (unsigned long long)__double_as_longlong(X[4 * q + 3]);
+    w0[0] = (unsigned)a0; w0[1] = (unsigned)(a0 >> 32); w0[2] = (unsigned)a1; w0[3] = (unsigned)(a1 >> 32);
+    w1[0] = (unsigned)b0; w1[1] = (unsigned)(b0 >> 32); w1[2] = (unsigned)b1; w1[3] = (unsigned)(b1 >> 32);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      v4u v;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const unsigned x0 = (unsigned)__builtin_amdgcn_ds_bpermute(src + 32 * h, (int)w0[d]);
+        const unsigned x1 = (unsigned)__builtin_amdgcn_ds_bpermute(src + 32 * h, (int)w1[d]);
+        v[d] = hi ? x1 : x0;
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, base, h * hoff + 128 * q, TQR_STRIP_ST_AUX);
+    }
+  }
+}
 // Head rows through a buffer resource (chain engine): base = byte offset of (row r0 + x,
 // column col0 + 4blk + y); soffset carries 4 rows per access. A resource with num_records = 0
 // makes every load return 0 and drops every store — the branch-free "no head" of the UNMQR

@@ -421,6 +421,16 @@ int main(int argc, char** argv) {
     if (run<40>(X, H, img, ncu, nelem, clk)) return 1;
     if (run<64>(X, H, img, ncu, nelem, clk)) return 1;
     if (run<72>(X, H, img, ncu, nelem, clk)) return 1;
+  } else if (sel == 6) {  // round 6: the late-load hand-over decomposed (stores dropped / loads zero / no strip
+                          // I/O), in lockstep and with the workgroups' hand-overs spread (desync)
+    if (run<264>(X, H, img, ncu, nelem, clk)) return 1;
+    if (run<264 + 16>(X, H, img, ncu, nelem, clk)) return 1;
+    if (run<264 + 32>(X, H, img, ncu, nelem, clk)) return 1;
+    if (run<264 + 1>(X, H, img, ncu, nelem, clk)) return 1;
+    if (run<264 + 64>(X, H, img, ncu, nelem, clk)) return 1;
+    if (run<264 + 64 + 16>(X, H, img, ncu, nelem, clk)) return 1;
+    if (run<264 + 64 + 32>(X, H, img, ncu, nelem, clk)) return 1;
+    if (run<264 + 64 + 1>(X, H, img, ncu, nelem, clk)) return 1;
   } else if (sel == 2) {  // late strip loads vs the whole strip in the hand-over
     if (run<8>(X, H, img, ncu, nelem, clk)) return 1;
     if (run<264>(X, H, img, ncu, nelem, clk)) return 1;
