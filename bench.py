@@ -31,6 +31,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -569,8 +570,22 @@ def main():
         del Ah, Th
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_sample, 256, f32=args.storage == "f32", target=(m, n),
-                           full_target=not args.no_full_cpu_target)
+        # (minutes of host work with no other output: a heartbeat on stderr every 30 s, the ctypes
+        # calls release the GIL; stdout carries the one result line only)
+        done = threading.Event()
+
+        def heartbeat():
+            t0 = time.perf_counter()
+            while not done.wait(30.0):
+                print(f"bench: cpu_baseline running ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
+        hb = threading.Thread(target=heartbeat, daemon=True)
+        hb.start()
+        try:
+            cpu = cpu_baseline(args.cpu_sample, 256, f32=args.storage == "f32", target=(m, n),
+                               full_target=not args.no_full_cpu_target)
+        finally:
+            done.set()
+            hb.join()
 
     cfg = 2 if (m, n) == (16384, 16384) else 3 if (m, n) == (65536, 16384) else 1 if (m, n) == (4096, 4096) else "custom"
     if args.storage == "f32":

@@ -13,7 +13,7 @@ if [ "${TESTS:-1}" = 1 ]; then
   tail -2 $OUT/pytest_gpu.log
 fi
 if [ "${BENCH:-1}" = 1 ]; then
-  timeout -k 10 400 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { echo "bench failed"; tail -20 $OUT/bench_default.err; exit 1; }
+  timeout -k 10 700 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { echo "bench failed"; tail -20 $OUT/bench_default.err; exit 1; }
   cat $OUT/bench_default.json
   timeout -k 10 400 python bench.py --storage f32 --rows 32768 --cols 32768 > $OUT/bench_f32_c5.json 2> $OUT/bench_f32_c5.err || { echo "bench f32 failed"; tail -20 $OUT/bench_f32_c5.err; exit 1; }
   cat $OUT/bench_f32_c5.json
