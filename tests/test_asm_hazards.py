@@ -97,6 +97,20 @@ def test_compiled_pairs_are_the_compilers():
     assert AH.check_text(_func(lines), all_pairs=True)["fn"]
 
 
+def test_store_war_soffset_register_exception():
+    """Hardware rule (--all): a >8-byte MUBUF store whose soffset is an SGPR has no data hazard (hipcc
+    pads none); with a constant soffset, or a global store, one wait state is needed."""
+    rd = ["v_cndmask_b32_e64 v0, v15, v14, s[72:73]"]
+    sgpr = ["<asm>", "buffer_store_dwordx4 v[0:3], v36, s[48:51], s68 offen sc1", "</asm>"]
+    const = ["<asm>", "buffer_store_dwordx4 v[0:3], v36, s[48:51], 0 offen sc1", "</asm>"]
+    glob = ["<asm>", "global_store_dwordx4 v[40:41], v[0:3], off sc1", "</asm>"]
+    assert not AH.check_text(_func(sgpr + rd), all_pairs=True)["fn"]
+    assert AH.check_text(_func(const + rd), all_pairs=True)["fn"]
+    assert AH.check_text(_func(glob + rd), all_pairs=True)["fn"]
+    # the generators' own margin (default mode) applies to every store
+    assert _violations(sgpr[:-1] + rd + ["</asm>"])
+
+
 def test_hazard_across_a_back_edge():
     """The pair is only formed around the loop: the statement's last MFMA, the next iteration's first read."""
     lines = [".LBB0_1:", "<asm>", "v_add_f64 v[112:113], v[112:113], v[80:81]", "s_nop 7",

@@ -347,6 +347,11 @@ def _advance(state, n):
     return out
 
 
+def _mubuf_soffset_reg(insn):
+    """A buffer_* store whose soffset operand (the 4th: vdata, vaddr, srsrc, soffset) is an SGPR."""
+    return insn.op.startswith("buffer_") and len(insn.ops) > 3 and re.match(r"s\d+$|s\[", insn.ops[3]) is not None
+
+
 def _store_bytes(op):
     m = re.search(r"_(?:dword|b)(x?\d*)$", op.split("_lds")[0])
     if op.endswith(("_dwordx4", "_b128")):
@@ -380,8 +385,11 @@ def _step(state, insn, report, hw=False):
                 report(insn, wline, w_asm, f"{w_cls} {w_op} -> {insn.op} ({role} {reg}): {dist} of {req} wait states")
     # write-after-read of a store's data VGPRs
     for reg in insn.writes:
-        for (r, w_cls, w_op), (dist, wline, w_asm, _) in by_reg.get(reg, []):
-            need = (HZ.STORE_WAR_HW if _store_bytes(w_op) > 8 and insn.cls != "load" else 0) if hw else HZ.STORE_WAR
+        for (r, w_cls, w_op), (dist, wline, w_asm, w_soff) in by_reg.get(reg, []):
+            # (hardware: a MUBUF store whose soffset is a register has no data hazard — the rule
+            # of LLVM's GCNHazardRecognizer::createsVALUHazard, which hipcc pads by)
+            need = (HZ.STORE_WAR_HW if _store_bytes(w_op) > 8 and insn.cls != "load" and not w_soff else 0) \
+                if hw else HZ.STORE_WAR
             if w_cls == "store_read" and insn.cls in ("valu", "mfma", "readlane", "load") and need > dist:
                 report(insn, wline, w_asm, f"store data {reg} of {w_op} overwritten by {insn.op}: {dist} of {need} wait states")
     state = _advance(state, insn.waits)
@@ -394,7 +402,7 @@ def _step(state, insn, report, hw=False):
             state[("__gpr_idx", "gpr_idx_on", insn.op)] = (0, insn.line, insn.in_asm, None)
         for reg, role in insn.reads:
             if role == "store_data":
-                state[(reg, "store_read", insn.op)] = (0, insn.line, insn.in_asm, None)
+                state[(reg, "store_read", insn.op)] = (0, insn.line, insn.in_asm, _mubuf_soffset_reg(insn))
     return state
 
 
