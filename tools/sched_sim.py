@@ -827,6 +827,14 @@ REH5 = [("1 rank x 256 (one GPU, c4)", 1, 256, "r4", 581.338),
         ("2 ranks x 128 (rehearsal)", 2, 128, "r4", 591.792),
         ("4 ranks x 64 (rehearsal)", 4, 64, "r4", 602.1),
         ("4 ranks x 64, 8-GPU list (rehearsal)", 4, 64, "r5", 621.778)]
+# the same shapes measured with the round-6 code on another box (profiles/r06/reh6, tools/reh_round.sh)
+REH6 = [("1 rank x 256 (one GPU, c4)", 1, 256, "r4", 587.183),
+        ("1 rank x 128 (t1 leg of the 2-rank run)", 1, 128, "r4", 1075.378),
+        ("1 rank x 64 (t1 leg of the 4-rank run)", 1, 64, "r4", 2084.127),
+        ("1 rank x 64, 8-GPU list (t1 leg)", 1, 64, "r5", 2180.608),
+        ("2 ranks x 128 (rehearsal)", 2, 128, "r4", 597.346),
+        ("4 ranks x 64 (rehearsal)", 4, 64, "r4", 608.097),
+        ("4 ranks x 64, 8-GPU list (rehearsal)", 4, 64, "r5", 632.334)]
 LISTS = {"r4": {"TQR_SEGLEN": "8"},  # (the rehearsals' ranks do not cover a device: segment length 8)
          "r4d": {"TQR_SEGLEN": "2"},  # round-4 multi-rank default: 2-element segments
          "r5": {"TQR_SEGLEN": "2", "TQR_TAIL": "28", "TQR_TAIL_SEGLEN": "1", "TQR_LAC": "4"}}  # round 5's
@@ -835,22 +843,24 @@ LISTS = {"r4": {"TQR_SEGLEN": "8"},  # (the rehearsals' ranks do not cover a dev
 def main_calib(argv):
     """The multi-GPU model against the round-5 one-GPU measurements (profiles/r05/reh5): per shape the
     model's time, the measured one, their ratio; then t(8) on 8 x 256 workgroups for the round-4 and
-    round-5 multi-rank task lists, corrected by the rehearsals' fitted ratio. Args: [M] [N]"""
+    round-5 multi-rank task lists, corrected by the rehearsals' fitted ratio. Args: [M] [N]
+    (TQR_CALIB_SET=reh6: the round-6 measurements instead)"""
     M, N = _mn(argv)
+    reh = REH6 if os.environ.get("TQR_CALIB_SET") == "reh6" else REH5
     seg = float(os.environ.get("TQR_SIM_SEG", "20"))
     prm = dict(P5, seg=seg)
     lists = {k: _list_env(v, M, N) for k, v in LISTS.items()}
     ratios = {}
     print(f"{M}x{N} tiles, round-5 costs, per-segment {seg} us", flush=True)
-    for name, world, W, lst, meas in REH5:
+    for name, world, W, lst, meas in reh:
         t = simulate_dist(lists[lst], M, N, world, prm=dict(prm, W=W)) / 1e3
         ratios[name] = meas / t
         print(f"  {name:42s} model {t:8.1f} ms  measured {meas:8.1f}  ratio {meas / t:5.3f}", flush=True)
-    reh = [ratios[n] for n, w, *_ in REH5 if w > 1]
-    one = ratios[REH5[0][0]]
-    lo, hi = min(reh), max(reh)
+    rr = [ratios[n] for n, w, *_ in reh if w > 1]
+    one = ratios[reh[0][0]]
+    lo, hi = min(rr), max(rr)
     print(f"  multi-rank rehearsals: measured / model {lo:.3f} .. {hi:.3f}; one GPU {one:.3f}")
-    t1 = REH5[0][4]
+    t1 = reh[0][4]
     for lst in ("r4d", "r5"):
         t8 = simulate_dist(lists[lst], M, N, 8, prm=dict(prm, W=256)) / 1e3
         print(f"  8 x 256, list {lst:3s}: model t(8) {t8:6.1f} ms, S(8) {t1 / t8:4.2f} uncorrected; corrected t(8) "
