@@ -996,6 +996,9 @@ __device__ __noinline__ void panel_factor(double* Vs, double* Hs, double* tauv, 
     for (int C = Q3; C < IB; ++C) panel_step<B, TS, IB / 4, IBX>(x, Vs, Hs, tauv, red, wb, hrow, hout, c0, C, own, rt PS_ARGS);
   }
   PS_FLUSH();
+#ifdef TQR_DIAG_PFSLOW  // what-if: the factorisation N x ~3.4 us slower per group (marginal sensitivity)
+  for (int i = 0; i < TQR_DIAG_PFSLOW; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
   __syncthreads();
   if (TS) {
     for (int idx = t; idx < IB * IB; idx += 256) {
